@@ -1,0 +1,333 @@
+"""Python host binding of the MI355X ray tracer (librt_hip.so, C-ABI in include/rt_abi.h).
+
+Mirrors the reference's host interface so a host written against it reads the same:
+
+* ``Scene``      -- RayTracing::Scene (RayTracing/Scene.h:87-129): AddTriangle/AddQuad/
+                    AddSphere/AddMaterial/AddLoadedScene, the camera, ``upload``.
+* ``RayTracer``  -- CUDARayTracer (RayTracing/RayTracing.{h,cpp}): owns the scene, the
+                    per-pixel RNG state and the progressive frame index; ``process()``
+                    renders one frame (RayTracing.cpp:205-234).
+* ``raytracing_process`` / ``init_rng`` -- the two extern "C" entry points
+                    (main_raytracing.cu:202, Random.cu:10).
+
+Device buffers are torch tensors on the current HIP device (torch is plumbing here: memory,
+streams, torch.distributed); every kernel is in librt_hip.so.  There is no CPU fallback: if
+the native library is missing or fails to load this module raises.
+"""
+import ctypes
+import os
+
+import torch  # imported first so librt_hip.so binds to the HIP runtime torch already loaded
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "librt_hip.so")
+ASSETS_DIR = os.path.join(ROOT_DIR, "assets")
+
+RT_RENDER_STATS = 1
+STAT_NAMES = ("segments", "nodes", "tri_tests", "tri_accepts", "sphere_accepts", "hits", "misses")
+SCENES = {"bunny": 0, "bunny4": 1, "plane1m": 2}
+
+REFERENCE_SPP = 5      # main_raytracing.cu:166-170 (Release)
+REFERENCE_BOUNCES = 6  # main_raytracing.cu:115
+RNG_STATE_BYTES = 48   # sizeof(curandState)
+
+
+class GPUCamera(ctypes.Structure):
+    _fields_ = [("origin", ctypes.c_float * 3), ("viewport_worldspace_size", ctypes.c_float * 2),
+                ("aspect", ctypes.c_float), ("horizontal", ctypes.c_float * 3),
+                ("vertical", ctypes.c_float * 3), ("lower_left_corner", ctypes.c_float * 3)]
+
+
+class GPUScene(ctypes.Structure):
+    _fields_ = [("gpu_spheres", ctypes.c_void_p), ("gpu_materials", ctypes.c_void_p),
+                ("gpu_bvh_nodes", ctypes.c_void_p), ("gpu_bvh_face_indices", ctypes.c_void_p),
+                ("gpu_vertices", ctypes.c_void_p), ("gpu_faces", ctypes.c_void_p),
+                ("sphere_count", ctypes.c_int32), ("material_count", ctypes.c_int32),
+                ("rng_state", ctypes.c_void_p), ("environment_cubemap_tex", ctypes.c_uint64),
+                ("camera", GPUCamera)]
+
+
+class GPUMaterial(ctypes.Structure):
+    _fields_ = [("albedo", ctypes.c_float * 4), ("emissive", ctypes.c_float * 4), ("specular", ctypes.c_float * 4),
+                ("roughness", ctypes.c_float), ("specular_percent", ctypes.c_float), ("IOR", ctypes.c_float),
+                ("_pad", ctypes.c_float)]
+
+
+class RenderParams(ctypes.Structure):
+    _fields_ = [("surface", ctypes.c_void_p), ("surface_last_frame", ctypes.c_void_p),
+                ("width", ctypes.c_int32), ("height", ctypes.c_int32), ("pitch", ctypes.c_uint64),
+                ("frame_index", ctypes.c_int32), ("spp", ctypes.c_int32), ("bounces", ctypes.c_int32),
+                ("shard_index", ctypes.c_int32), ("shard_count", ctypes.c_int32), ("flags", ctypes.c_int32),
+                ("out_shard", ctypes.c_void_p), ("stats", ctypes.c_void_p), ("segment_counter", ctypes.c_void_p)]
+
+
+assert ctypes.sizeof(GPUScene) == 136 and ctypes.sizeof(GPUMaterial) == 64
+
+# name -> (restype, argtypes); every symbol include/rt_abi.h declares.
+_P, _I, _U32, _U64, _F, _SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_size_t
+_FP = ctypes.POINTER(ctypes.c_float)
+SIGNATURES = {
+    "raytracing_process": (None, [_P, _P, _I, _I, _SZ, _I, _P]),
+    "init_rng": (None, [_U32, _U32, _P, ctypes.c_uint]),
+    "rt_render": (_I, [ctypes.POINTER(RenderParams), _P, _P]),
+    "rt_init_rng": (_I, [_P, _I, _I, _I, _I, _U32, _P]),
+    "rt_shard_tiles": (ctypes.c_int64, [_I, _I, _I, _I]),
+    "rt_unshard": (_I, [_P, _U64, _I, _I, _I, _P, ctypes.c_int64, _P]),
+    "rt_set_device": (_I, [_I]),
+    "rt_malloc": (_I, [ctypes.POINTER(_P), _SZ]),
+    "rt_malloc_pitch": (_I, [ctypes.POINTER(_P), ctypes.POINTER(_SZ), _SZ, _SZ]),
+    "rt_free": (_I, [_P]),
+    "rt_memcpy_h2d": (_I, [_P, _P, _SZ]),
+    "rt_memcpy_d2h": (_I, [_P, _P, _SZ]),
+    "rt_memcpy_d2d": (_I, [_P, _P, _SZ]),
+    "rt_memset": (_I, [_P, _I, _SZ]),
+    "rt_synchronize": (_I, []),
+    "rt_last_error": (ctypes.c_char_p, []),
+    "rt_cubemap_create": (_U64, [_FP, _I]),
+    "rt_cubemap_destroy": (_I, [_U64]),
+    "rt_scene_create": (_P, []),
+    "rt_scene_destroy": (None, [_P]),
+    "rt_scene_add_material": (_U32, [_P, ctypes.POINTER(GPUMaterial)]),
+    "rt_scene_add_triangle": (None, [_P, _FP, _FP, _FP, _I]),
+    "rt_scene_add_quad": (None, [_P, _FP, _FP, _FP, _FP, _I]),
+    "rt_scene_add_sphere": (None, [_P, _FP, _F, _I]),
+    "rt_scene_add_mesh_file": (_I, [_P, ctypes.c_char_p, _FP, _I]),
+    "rt_scene_set_environment_file": (_I, [_P, ctypes.c_char_p]),
+    "rt_scene_set_camera": (None, [_P, _FP, _F, _F]),
+    "rt_scene_set_viewport": (None, [_P, _I, _I]),
+    "rt_scene_upload": (_I, [_P, _P]),
+    "rt_scene_gpu": (ctypes.POINTER(GPUScene), [_P]),
+    "rt_scene_setup": (_I, [_P, _I, ctypes.c_char_p]),
+    "rt_scene_setup_plane": (_I, [_P, _I, ctypes.c_char_p]),
+    "rt_scene_build": (None, [_P]),
+    "rt_scene_camera": (None, [_P, ctypes.POINTER(GPUCamera)]),
+    "rt_scene_host_arrays": (_SZ, [_P, ctypes.POINTER(_P), ctypes.POINTER(_SZ), ctypes.POINTER(_P),
+                                   ctypes.POINTER(_SZ), ctypes.POINTER(_P), ctypes.POINTER(_SZ), ctypes.POINTER(_P)]),
+    "rt_scene_bvh_max_depth": (_I, [_P]),
+    "rt_xorwow_jump_matrix": (_I, [_I, ctypes.POINTER(ctypes.c_uint32)]),
+    "rt_xorwow_init_host": (None, [_U32, _U64, _P]),
+}
+
+_lib = None
+
+
+class RTError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load librt_hip.so (raises if it is missing: there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RTError(f"{LIB_PATH} not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(code, what):
+    if code:
+        raise RTError(f"{what} failed ({code}): {lib().rt_last_error().decode(errors='replace')}")
+
+
+def _f3(v):
+    return (ctypes.c_float * 3)(*[float(x) for x in v])
+
+
+def _stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class Scene:
+    """RayTracing::Scene mirror (RayTracing/Scene.h:87-129)."""
+
+    def __init__(self):
+        self.handle = lib().rt_scene_create()
+        if not self.handle:
+            raise RTError("rt_scene_create failed")
+
+    def __del__(self):
+        if getattr(self, "handle", None) and _lib is not None:
+            _lib.rt_scene_destroy(self.handle)
+            self.handle = None
+
+    # --- building (Scene.cpp:46-139) -------------------------------------------------
+    def add_material(self, albedo=(0, 0, 0), emissive=(0, 0, 0), specular=(0, 0, 0, 0), roughness=0.9,
+                     specular_percent=0.0, ior=1.0):
+        m = GPUMaterial()
+        m.albedo[:] = [*map(float, albedo[:3]), 1.0]
+        m.emissive[:] = [*map(float, emissive[:3]), 1.0]
+        m.specular[:] = [*map(float, (list(specular) + [0.0])[:4])]
+        m.roughness, m.specular_percent, m.IOR = roughness, specular_percent, ior
+        return lib().rt_scene_add_material(self.handle, ctypes.byref(m))
+
+    def add_triangle(self, a, b, c, material=0):
+        lib().rt_scene_add_triangle(self.handle, _f3(a), _f3(b), _f3(c), material)
+
+    def add_quad(self, a, b, c, d, material=0):
+        lib().rt_scene_add_quad(self.handle, _f3(a), _f3(b), _f3(c), _f3(d), material)
+
+    def add_sphere(self, position, radius, material=0):
+        lib().rt_scene_add_sphere(self.handle, _f3(position), float(radius), material)
+
+    def add_loaded_scene(self, mesh_path, transform, material=0):
+        t = (ctypes.c_float * 16)(*[float(x) for x in transform])
+        _check(lib().rt_scene_add_mesh_file(self.handle, mesh_path.encode(), t, material), "add_loaded_scene")
+
+    def set_environment(self, path):
+        _check(lib().rt_scene_set_environment_file(self.handle, path.encode()), "set_environment")
+
+    def setup(self, which="bunny", assets_dir=ASSETS_DIR):
+        """CUDARayTracer::SetupCornellBox + SetupStanfordBunny (or the config-4/5 scenes)."""
+        _check(lib().rt_scene_setup(self.handle, SCENES[which], assets_dir.encode()), f"setup({which})")
+
+    def setup_plane(self, n=708, assets_dir=ASSETS_DIR):
+        _check(lib().rt_scene_setup_plane(self.handle, int(n), assets_dir.encode()), f"setup_plane({n})")
+
+    def set_camera(self, position=(0, 0, 0), angle_x=0.0, angle_y=180.0):
+        lib().rt_scene_set_camera(self.handle, _f3(position), float(angle_x), float(angle_y))
+
+    def set_viewport(self, width, height):
+        lib().rt_scene_set_viewport(self.handle, int(width), int(height))
+
+    def upload(self, rng_state_ptr):
+        """Scene::Upload (Scene.cpp:182-234): BVH build if dirty, H2D copies, GPUScene fill."""
+        _check(lib().rt_scene_upload(self.handle, ctypes.c_void_p(rng_state_ptr)), "upload")
+
+    @property
+    def gpu(self):
+        return lib().rt_scene_gpu(self.handle)
+
+    def build(self):
+        """Host half of upload (camera + BVH) with no device work."""
+        lib().rt_scene_build(self.handle)
+
+    def camera(self):
+        c = GPUCamera()
+        lib().rt_scene_camera(self.handle, ctypes.byref(c))
+        return c
+
+    def max_depth(self):
+        return lib().rt_scene_bvh_max_depth(self.handle)
+
+    def host_arrays(self):
+        """numpy copies of the host arrays: nodes (N,8) f32/u32 view, face indices, vertices, faces."""
+        import numpy as np
+        ptrs = [ctypes.c_void_p() for _ in range(4)]
+        counts = [ctypes.c_size_t() for _ in range(3)]
+        lib().rt_scene_host_arrays(self.handle, ctypes.byref(ptrs[0]), ctypes.byref(counts[0]), ctypes.byref(ptrs[1]),
+                                   ctypes.byref(counts[1]), ctypes.byref(ptrs[2]), ctypes.byref(counts[2]),
+                                   ctypes.byref(ptrs[3]))
+
+        def grab(p, nbytes):
+            if not p.value or nbytes == 0:
+                return np.zeros(0, dtype=np.uint8)
+            return np.frombuffer(ctypes.string_at(p.value, nbytes), dtype=np.uint8).copy()
+
+        nn, nf, nv = counts[0].value, counts[1].value, counts[2].value
+        return {"nodes": grab(ptrs[0], nn * 32), "face_indices": grab(ptrs[1], nf * 4),
+                "vertices": grab(ptrs[2], nv * 32), "faces": grab(ptrs[3], nf * 16)}
+
+
+def alloc_surface(width, height, device=None):
+    """A pitched float4 surface (RGBA fp32), rows padded to a 256-byte pitch like cudaMallocPitch."""
+    row_floats = ((width * 16 + 255) // 256) * 256 // 4
+    t = torch.zeros((height, row_floats), dtype=torch.float32, device=device or "cuda")
+    return t
+
+
+def surface_view(t, width):
+    """[H, W, 4] view of a pitched surface tensor."""
+    return t[:, : width * 4].reshape(t.shape[0], width, 4)
+
+
+def alloc_rng(count, device=None):
+    return torch.zeros((count * RNG_STATE_BYTES // 4,), dtype=torch.int32, device=device or "cuda")
+
+
+def init_rng_states(rng, width, height, seed, shard_index=0, shard_count=1, stream=None):
+    _check(lib().rt_init_rng(ctypes.c_void_p(rng.data_ptr()), width, height, shard_index, shard_count, seed,
+                             _stream_ptr(stream)), "rt_init_rng")
+
+
+def render(scene, surface, last, width, height, spp, bounces, frame_index=0, shard_index=0, shard_count=1,
+           out_shard=None, stats=None, segment_counter=None, stream=None):
+    """rt_render: one frame (or one shard of it) on `stream` (default: torch's current stream)."""
+    p = RenderParams()
+    p.surface = surface.data_ptr() if surface is not None else None
+    p.surface_last_frame = last.data_ptr() if last is not None else None
+    p.width, p.height = width, height
+    p.pitch = surface.shape[1] * 4 if surface is not None else width * 16
+    p.frame_index, p.spp, p.bounces = frame_index, spp, bounces
+    p.shard_index, p.shard_count = shard_index, shard_count
+    p.out_shard = out_shard.data_ptr() if out_shard is not None else None
+    if segment_counter is not None:
+        p.segment_counter = segment_counter.data_ptr()
+    if stats is not None:
+        p.flags = RT_RENDER_STATS
+        p.stats = stats.data_ptr()
+    _check(lib().rt_render(ctypes.byref(p), ctypes.cast(scene.gpu, ctypes.c_void_p), _stream_ptr(stream)), "rt_render")
+
+
+def shard_tiles(width, height, shard_index, shard_count):
+    return int(lib().rt_shard_tiles(width, height, shard_index, shard_count))
+
+
+def unshard(surface, width, height, shard_count, shards, per_shard, stream=None):
+    _check(lib().rt_unshard(ctypes.c_void_p(surface.data_ptr()), surface.shape[1] * 4, width, height, shard_count,
+                            ctypes.c_void_p(shards.data_ptr()), per_shard, _stream_ptr(stream)), "rt_unshard")
+
+
+def raytracing_process(surface, last, width, height, frame_index, scene):
+    """The reference entry point (main_raytracing.cu:202): spp 5, 6 bounces, null stream."""
+    lib().raytracing_process(ctypes.c_void_p(surface.data_ptr()), ctypes.c_void_p(last.data_ptr()), width, height,
+                             surface.shape[1] * 4, frame_index, ctypes.cast(scene.gpu, ctypes.c_void_p))
+
+
+def init_rng(thread_block_count, thread_block_size, rng, seed):
+    """The reference entry point (Random.cu:10)."""
+    lib().init_rng(thread_block_count, thread_block_size, ctypes.c_void_p(rng.data_ptr()), seed)
+
+
+class RayTracer:
+    """CUDARayTracer mirror (RayTracing/RayTracing.{h,cpp}), headless.
+
+    ``process()`` = one progressive frame: lazy RNG init (fixed seed instead of the
+    reference's time-based one), camera update + upload, render, copy to the last-frame
+    surface, frame_index++ (RayTracing.cpp:205-234).
+    """
+
+    def __init__(self, width, height, scene="bunny", spp=REFERENCE_SPP, bounces=REFERENCE_BOUNCES, seed=0xDEADBEEF):
+        self.width, self.height, self.spp, self.bounces, self.seed = width, height, spp, bounces, seed
+        self.scene = Scene()
+        self.scene.setup(scene)
+        self.surface = alloc_surface(width, height)
+        self.last_frame = alloc_surface(width, height)
+        self.rng = None
+        self.frame_index = 0
+
+    def on_resize(self, width, height):
+        self.width, self.height = width, height
+        self.surface = alloc_surface(width, height)
+        self.last_frame = alloc_surface(width, height)
+        self.rng = None
+        self.frame_index = 0
+
+    def process(self, stats=None):
+        if self.rng is None:
+            self.rng = alloc_rng(self.width * self.height)
+            init_rng_states(self.rng, self.width, self.height, self.seed)
+        self.scene.set_viewport(self.width, self.height)
+        self.scene.upload(self.rng.data_ptr())
+        render(self.scene, self.surface, self.last_frame, self.width, self.height, self.spp, self.bounces,
+               frame_index=self.frame_index, stats=stats)
+        self.last_frame.copy_(self.surface)
+        self.frame_index += 1
+        return surface_view(self.surface, self.width)

@@ -1,0 +1,90 @@
+"""Build the native pieces of this repository.
+
+librt_hip.so   cuda-raytracing_amd/csrc  -> the product: HIP kernels for gfx950 + the C-ABI shim
+               + the C++ host scene/BVH mirror (one shared library, include/rt_abi.h).
+liboracle.so   oracle/rt_oracle.c        -> the CPU restatement used only by tests, smoke() and
+               bench.py's cpu_baseline leg (gcc, OpenMP, -ffp-contract=off).
+
+Both are built in-tree so the built .so files travel to the GPU box with the repo snapshot.
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "cuda-raytracing_amd")
+CSRC = os.path.join(PKG, "csrc")
+INC = os.path.join(ROOT, "include")
+BUILD = os.path.join(PKG, "build")
+LIB = os.path.join(PKG, "librt_hip.so")
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
+
+# Numerics flags shared by every translation unit of the product: no FMA contraction, IEEE
+# fp32 division and square root (bit-exact agreement between host code, kernels and oracle).
+FP_FLAGS = ["-ffp-contract=off", "-fno-fast-math"]
+HOST_SOURCES = ["scene.cpp", "xorwow.cpp"]
+HIP_SOURCES = ["rt_kernel.hip"]
+
+
+def _run(cmd):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return False
+    t = os.path.getmtime(target)
+    return all(os.path.getmtime(d) <= t for d in deps)
+
+
+def _deps(dirpath, exts):
+    return [os.path.join(dirpath, f) for f in os.listdir(dirpath) if f.endswith(exts)]
+
+
+def build_product(force=False):
+    os.makedirs(BUILD, exist_ok=True)
+    deps = _deps(CSRC, (".h", ".hip", ".cpp")) + _deps(INC, (".h",)) + [os.path.abspath(__file__)]
+    if not force and _newer(LIB, deps):
+        return LIB
+    objs = []
+    for src in HIP_SOURCES:
+        obj = os.path.join(BUILD, src + ".o")
+        _run([HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *FP_FLAGS,
+              "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics", "-I", INC, "-I", CSRC,
+              "-c", os.path.join(CSRC, src), "-o", obj])
+        objs.append(obj)
+    for src in HOST_SOURCES:
+        obj = os.path.join(BUILD, src + ".o")
+        _run(["g++", "-O2", "-std=c++17", "-fPIC", *FP_FLAGS, "-I", INC, "-I", CSRC,
+              "-c", os.path.join(CSRC, src), "-o", obj])
+        objs.append(obj)
+    tmp = LIB + ".tmp"
+    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp])
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def build_oracle(force=False):
+    src = os.path.join(ORACLE_DIR, "rt_oracle.c")
+    deps = [src, os.path.abspath(__file__)] + _deps(ORACLE_DIR, (".h",))
+    if not force and _newer(ORACLE_LIB, deps):
+        return ORACLE_LIB
+    tmp = ORACLE_LIB + ".tmp"
+    _run(["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-fopenmp", *FP_FLAGS, src, "-o", tmp, "-lm"])
+    os.replace(tmp, ORACLE_LIB)
+    return ORACLE_LIB
+
+
+def build_all(force=False):
+    build_product(force)
+    build_oracle(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

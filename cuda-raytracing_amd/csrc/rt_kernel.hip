@@ -1,0 +1,557 @@
+// rt_kernel.hip -- MI355X (gfx950) render path behind the C-ABI of include/rt_abi.h.
+//
+// Kernels
+//   render_kernel<STACK, STATS>  per-pixel path tracer (RayTracing/main_raytracing.cu:33-200):
+//       one 256-thread workgroup per 16x16 pixel tile, each wave64 an 8x8 sub-tile (ray
+//       coherence inside a wave), per-thread BVH stack in LDS laid out [entry][thread] so
+//       the 64 lanes of a push/pop hit 64 consecutive dwords (conflict-free), RNG state in
+//       registers for the whole pixel (one 24-B read and one 24-B write per pixel instead
+//       of a global read-modify-write per draw).
+//   init_rng_kernel              curand_init(seed, pixel, 0) with GF(2) jump matrices.
+//   unshard_kernel               scatter gathered tile shards back into a pitched surface.
+//
+// Numerics: compiled with -ffp-contract=off and IEEE fp32 division/sqrt, so every value
+// matches the CPU oracle bit for bit ("Parity").
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+
+#include "rt_abi.h"
+#include "rt_device.h"
+#include "rt_math.h"
+#include "xorwow.h"
+
+int rt_internal_lookup_depth(const void* gpu_nodes);
+
+// ---------------------------------------------------------------------------------------
+// error state
+// ---------------------------------------------------------------------------------------
+static thread_local std::string g_last_error;
+
+static int set_error(const std::string& msg, int code = 1) {
+    g_last_error = msg;
+    return code;
+}
+static int check(hipError_t e, const char* what) {
+    if (e == hipSuccess) return 0;
+    return set_error(std::string(what) + ": " + hipGetErrorString(e), (int)e);
+}
+
+extern "C" const char* rt_last_error(void) { return g_last_error.c_str(); }
+
+// ---------------------------------------------------------------------------------------
+// memory shim (utils/CUDAHelper.h:114-156)
+// ---------------------------------------------------------------------------------------
+extern "C" int rt_set_device(int device) { return check(hipSetDevice(device), "hipSetDevice"); }
+extern "C" int rt_malloc(void** ptr, size_t bytes) { return check(hipMalloc(ptr, bytes), "hipMalloc"); }
+extern "C" int rt_malloc_pitch(void** ptr, size_t* pitch, size_t width_bytes, size_t height) {
+    return check(hipMallocPitch(ptr, pitch, width_bytes, height), "hipMallocPitch");
+}
+extern "C" int rt_free(void* ptr) { return check(hipFree(ptr), "hipFree"); }
+extern "C" int rt_memcpy_h2d(void* dst, const void* src, size_t n) {
+    return check(hipMemcpy(dst, src, n, hipMemcpyHostToDevice), "hipMemcpy H2D");
+}
+extern "C" int rt_memcpy_d2h(void* dst, const void* src, size_t n) {
+    return check(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost), "hipMemcpy D2H");
+}
+extern "C" int rt_memcpy_d2d(void* dst, const void* src, size_t n) {
+    return check(hipMemcpy(dst, src, n, hipMemcpyDeviceToDevice), "hipMemcpy D2D");
+}
+extern "C" int rt_memset(void* dst, int value, size_t n) { return check(hipMemset(dst, value, n), "hipMemset"); }
+extern "C" int rt_synchronize(void) { return check(hipDeviceSynchronize(), "hipDeviceSynchronize"); }
+
+// ---------------------------------------------------------------------------------------
+// cube maps (utils/CUDATexture.cpp): a handle is the device address of float4[6][n][n]
+// ---------------------------------------------------------------------------------------
+static std::mutex g_cube_mutex;
+static std::map<uint64_t, int> g_cube_size;
+
+extern "C" uint64_t rt_cubemap_create(const float* rgba, int size) {
+    if (!rgba || size <= 0) {
+        set_error("rt_cubemap_create: bad arguments");
+        return 0;
+    }
+    void* p = nullptr;
+    const size_t bytes = (size_t)6 * size * size * 16;
+    if (rt_malloc(&p, bytes) || rt_memcpy_h2d(p, rgba, bytes)) return 0;
+    std::lock_guard<std::mutex> lock(g_cube_mutex);
+    g_cube_size[(uint64_t)p] = size;
+    return (uint64_t)p;
+}
+
+extern "C" int rt_cubemap_destroy(uint64_t handle) {
+    {
+        std::lock_guard<std::mutex> lock(g_cube_mutex);
+        if (!g_cube_size.erase(handle)) return set_error("rt_cubemap_destroy: unknown handle");
+    }
+    return rt_free((void*)handle);
+}
+
+static int cube_size(uint64_t handle) {
+    std::lock_guard<std::mutex> lock(g_cube_mutex);
+    auto it = g_cube_size.find(handle);
+    return it == g_cube_size.end() ? -1 : it->second;
+}
+
+// ---------------------------------------------------------------------------------------
+// render kernel
+// ---------------------------------------------------------------------------------------
+namespace {
+
+constexpr int TILE = 16;
+constexpr int BLOCK = 256;
+
+struct RenderArgs {
+    const GeometrySphere* spheres;
+    const GPUMaterial* materials;
+    const GPUBVHNode* nodes;
+    const uint32_t* face_indices;
+    const GPUVertex* vertices;
+    const GPUFace* faces;
+    rt_rng_state* rng;
+    const float* sky;  // float4 [6][n][n] or null
+    int sky_n;
+    int sphere_count;
+    GPUCamera cam;
+    float qw, qx, qy, qz;  // quat(vec3(0, PI, 0)) for the sky lookup (main_raytracing.cu:151)
+    char* surface;
+    const char* last;
+    float4* out_shard;
+    uint64_t pitch;
+    int width, height, frame_index, spp, bounces;
+    int shard_index, shard_count, tiles_x;
+    unsigned long long* stats;
+    unsigned long long* seg_counter;
+};
+
+__device__ __forceinline__ rtm::f3 ld3(const float* p) { return rtm::f3{p[0], p[1], p[2]}; }
+
+// Tile-local pixel of thread `tid`: wave w covers the 8x8 sub-tile ((w&1)*8, (w>>1)*8).
+__device__ __forceinline__ void tile_pixel(int tid, int* lx, int* ly) {
+    const int w = tid >> 6, l = tid & 63;
+    *lx = (w & 1) * 8 + (l & 7);
+    *ly = (w >> 1) * 8 + (l >> 3);
+}
+
+template <int STACK, bool STATS>
+__global__ __launch_bounds__(BLOCK) void render_kernel(RenderArgs a) {
+    __shared__ uint32_t stack_lds[STACK * BLOCK];
+    uint32_t* const stk = stack_lds + threadIdx.x;
+
+    const int tile = a.shard_index + (int)blockIdx.x * a.shard_count;
+    int lx, ly;
+    tile_pixel(threadIdx.x, &lx, &ly);
+    const int x = (tile % a.tiles_x) * TILE + lx;
+    const int y = (tile / a.tiles_x) * TILE + ly;
+    unsigned long long n_seg = 0, n_node = 0, n_tri = 0, n_tacc = 0, n_sacc = 0, n_hit = 0, n_miss = 0;
+    // Off-frame lanes of edge tiles skip the work but stay for the wave reduction below.
+    if (x < a.width && y < a.height) {
+    const size_t rng_index =
+        a.shard_count == 1 ? (size_t)y * a.width + x : (size_t)blockIdx.x * BLOCK + threadIdx.x;
+    rt_rng_state* rs = a.rng + rng_index;
+    rtm::Xorwow rng{rs->d, rs->v[0], rs->v[1], rs->v[2], rs->v[3], rs->v[4]};
+
+    const rtm::f3 cam_o = ld3(a.cam.origin), cam_h = ld3(a.cam.horizontal), cam_v = ld3(a.cam.vertical),
+                  cam_ll = ld3(a.cam.lower_left_corner);
+    float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f, acc_a = 0.0f;
+
+    for (int sample = 0; sample < a.spp; sample++) {
+        // main_raytracing.cu:190: uv = (pixel + vec2(rng(), rng())) / vec2(W, H), u drawn first
+        const float ru = rng.uniform();
+        const float rv = rng.uniform();
+        const float uvx = ((float)x + ru) / (float)a.width;
+        const float uvy = ((float)y + rv) / (float)a.height;
+        // GPUCamera::GetRay (GPUScene.h:13): llc + u*h + v*v - origin (not normalized)
+        rtm::f3 ro = cam_o;
+        rtm::f3 rd = rtm::sub(rtm::add(rtm::add(cam_ll, rtm::muls(cam_h, uvx)), rtm::muls(cam_v, uvy)), cam_o);
+
+        // ray_color (main_raytracing.cu:111-160)
+        rtm::f3 color = rtm::mk(0, 0, 0), thr = rtm::mk(1, 1, 1);
+        for (int bounce = 0; bounce < a.bounces; bounce++) {
+            n_seg++;
+            // GetRayHit (main_raytracing.cu:83-109)
+            const rtm::f3 nd = rtm::normalize(rd);
+            float best = 1e30f;
+            int hit_kind = 0;  // 0 none, 1 sphere, 2 triangle
+            uint32_t hit_id = 0;
+            float hbx = 0.0f, hby = 0.0f;
+            for (int i = 0; i < a.sphere_count; i++) {
+                const GeometrySphere& sp = a.spheres[i];
+                float dist;
+                if (rtd::intersect_sphere(ro, nd, ld3(sp.position), sp.radius * sp.radius, &dist)) {
+                    if (dist >= best) continue;
+                    best = dist;
+                    hit_kind = 1;
+                    hit_id = (uint32_t)i;
+                    if (STATS) n_sacc++;
+                }
+            }
+            // BVHRayHit (main_raytracing.cu:33-81): DFS, right child popped first
+            int sp_top = 0;
+            stk[0] = 0u;
+            sp_top = 1;
+            while (sp_top) {
+                const GPUBVHNode& node = a.nodes[stk[(--sp_top) * BLOCK]];
+                if (STATS) n_node++;
+                if (!rtd::intersect_aabb(ro, rd, node.bmin, node.bmax, best)) continue;
+                if (node.prim_count > 0) {
+                    for (uint32_t i = 0; i < node.prim_count; i++) {
+                        const uint32_t fi = a.face_indices[node.first_index + i];
+                        const GPUFace f = a.faces[fi];
+                        float bx, by, dist;
+                        if (STATS) n_tri++;
+                        if (rtd::intersect_triangle(ro, nd, ld3(a.vertices[f.v0].position), ld3(a.vertices[f.v1].position),
+                                                    ld3(a.vertices[f.v2].position), &bx, &by, &dist)) {
+                            if (dist >= best || dist < 0.0f) continue;
+                            best = dist;
+                            hit_kind = 2;
+                            hit_id = fi;
+                            hbx = bx;
+                            hby = by;
+                            if (STATS) n_tacc++;
+                        }
+                    }
+                } else {
+                    stk[(sp_top++) * BLOCK] = node.first_index;
+                    stk[(sp_top++) * BLOCK] = node.first_index + 1;
+                }
+            }
+
+            if (hit_kind != 0) {
+                if (STATS) n_hit++;
+                // Hit attributes of the final closest hit (the reference recomputes them on
+                // every accept; only the last accept survives).
+                const rtm::f3 pos = rtm::add(ro, rtm::muls(nd, best));
+                rtm::f3 nrm;
+                uint32_t mat;
+                if (hit_kind == 1) {
+                    const GeometrySphere& sp = a.spheres[hit_id];
+                    nrm = rtm::divs(rtm::sub(pos, ld3(sp.position)), sp.radius);
+                    mat = (uint32_t)sp.material;
+                } else {
+                    const GPUFace f = a.faces[hit_id];
+                    const float bz = (1.0f - hbx) - hby;
+                    nrm = rtm::normalize(rtm::add(rtm::add(rtm::muls(ld3(a.vertices[f.v0].normal), hbx),
+                                                           rtm::muls(ld3(a.vertices[f.v1].normal), hby)),
+                                                  rtm::muls(ld3(a.vertices[f.v2].normal), bz)));
+                    if (rtm::dot(nd, nrm) >= 0.0f) nrm = rtm::neg(nrm);
+                    mat = f.material;
+                }
+                const GPUMaterial& m = a.materials[mat];
+                const float do_spec = (rng.uniform() < m.specular_percent) ? 1.0f : 0.0f;
+                color = rtm::add(color, rtm::mul(thr, ld3(m.emissive)));
+                const float om = 1.0f - do_spec;
+                thr = rtm::mul(thr, rtm::mk(m.albedo[0] * om + m.specular[0] * do_spec,
+                                            m.albedo[1] * om + m.specular[1] * do_spec,
+                                            m.albedo[2] * om + m.specular[2] * do_spec));
+                // GetRandomPointOnSphere (Random.h:23-46)
+                const float zz = rng.uniform() * 2.0f - 1.0f;
+                const float ang = rng.uniform() * 3.141592654f * 2.0f;
+                const float rr = sqrtf(1.0f - zz * zz);
+                const rtm::f3 sph = rtm::mk(rr * rtm::rt_cosf(ang), rr * rtm::rt_sinf(ang), zz);
+                const rtm::f3 diffuse = rtm::normalize(rtm::add(nrm, sph));
+                rtm::f3 spec = rtm::normalize(rtm::reflect(rd, nrm));
+                spec = rtm::normalize(rtm::mix(spec, diffuse, m.roughness * m.roughness));
+                const rtm::f3 ndir = rtm::normalize(rtm::add(rtm::muls(diffuse, om), rtm::muls(spec, do_spec)));
+                ro = rtm::add(pos, rtm::muls(nrm, 0.01f));
+                rd = ndir;
+                // Russian roulette (main_raytracing.cu:140-148)
+                const float p = rtm::gmax(thr.x, rtm::gmax(thr.y, thr.z));
+                if (rng.uniform() > p) break;
+                thr = rtm::muls(thr, 1.0f / p);
+            } else {
+                if (STATS) n_miss++;
+                if (a.sky) {
+                    const rtm::f3 dir = rtd::quat_rotate(a.qw, a.qx, a.qy, a.qz, rd);
+                    const rtm::f3 c = rtd::cube_sample(a.sky, a.sky_n, dir);
+                    const rtm::f3 cl = rtm::mk(rtm::gmin(rtm::gmax(c.x, 0.0f), 50.0f), rtm::gmin(rtm::gmax(c.y, 0.0f), 50.0f),
+                                               rtm::gmin(rtm::gmax(c.z, 0.0f), 50.0f));
+                    color = rtm::add(color, rtm::mul(thr, cl));
+                }
+                break;
+            }
+        }
+        acc_r += color.x;
+        acc_g += color.y;
+        acc_b += color.z;
+        acc_a += 1.0f;
+    }
+
+    // main_raytracing.cu:195-199
+    const float fs = (float)a.spp;
+    const rtm::f4 res{acc_r / fs, acc_g / fs, acc_b / fs, acc_a / fs};
+    const float lerp = a.frame_index > 0 ? 1.0f / (float)(a.frame_index + 1) : 1.0f;
+    float4 prev;
+    float4* out;
+    if (a.out_shard) {
+        const size_t slot = (size_t)blockIdx.x * BLOCK + threadIdx.x;
+        prev = a.last ? reinterpret_cast<const float4*>(a.last)[slot] : make_float4(0, 0, 0, 0);
+        out = a.out_shard + slot;
+    } else {
+        prev = a.last ? *reinterpret_cast<const float4*>(a.last + (size_t)y * a.pitch + (size_t)x * 16)
+                      : make_float4(0, 0, 0, 0);
+        out = reinterpret_cast<float4*>(a.surface + (size_t)y * a.pitch + (size_t)x * 16);
+    }
+    const rtm::f4 o = rtm::mix4(rtm::f4{prev.x, prev.y, prev.z, prev.w}, res, lerp);
+    *out = make_float4(o.x, o.y, o.z, 1.0f);
+
+    rs->d = rng.d;
+    rs->v[0] = rng.v0;
+    rs->v[1] = rng.v1;
+    rs->v[2] = rng.v2;
+    rs->v[3] = rng.v3;
+    rs->v[4] = rng.v4;
+
+    }  // active pixel
+
+    // Segment count (always on: the Mrays/s numerator), one atomic per wave.
+    if (a.seg_counter) {
+        unsigned long long v = n_seg;
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if ((threadIdx.x & 63) == 0) atomicAdd(a.seg_counter, v);
+    }
+    if (STATS) {
+        atomicAdd(a.stats + RT_STAT_SEGMENTS, n_seg);
+        atomicAdd(a.stats + RT_STAT_NODES, n_node);
+        atomicAdd(a.stats + RT_STAT_TRI_TESTS, n_tri);
+        atomicAdd(a.stats + RT_STAT_TRI_ACCEPTS, n_tacc);
+        atomicAdd(a.stats + RT_STAT_SPHERE_ACCEPTS, n_sacc);
+        atomicAdd(a.stats + RT_STAT_HITS, n_hit);
+        atomicAdd(a.stats + RT_STAT_MISSES, n_miss);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// init_rng (Random.cu:3-13): state s <- curand_init(seed, pixel(s), 0)
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(BLOCK) void init_rng_kernel(rt_rng_state* states, const uint32_t* __restrict__ jump,
+                                                         uint32_t seed, int64_t count, int width, int height,
+                                                         int shard_index, int shard_count, int tiles_x) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= count) return;
+    uint64_t sub;
+    if (shard_count <= 0) {
+        sub = (uint64_t)s;  // reference layout: thread id == state index
+    } else {
+        const int64_t k = s / BLOCK;
+        const int tile = shard_index + (int)k * shard_count;
+        int lx, ly;
+        tile_pixel((int)(s % BLOCK), &lx, &ly);
+        const int x = (tile % tiles_x) * TILE + lx, y = (tile / tiles_x) * TILE + ly;
+        if (x >= width || y >= height) return;
+        sub = (uint64_t)y * (uint64_t)width + (uint64_t)x;
+    }
+    uint32_t st[6];
+    rt_xorwow_seed(seed, st);
+    uint32_t v[5] = {st[1], st[2], st[3], st[4], st[5]};
+    for (int k = 0; sub && k < RT_XORWOW_JUMPS; k++, sub >>= 2) {
+        const uint32_t reps = (uint32_t)(sub & 3u);
+        const uint32_t* m = jump + (size_t)k * 800;
+        for (uint32_t r = 0; r < reps; r++) {
+            uint32_t o[5] = {0, 0, 0, 0, 0};
+            for (int i = 0; i < 5; i++) {
+                const uint32_t word = v[i];
+                for (int j = 0; j < 32; j++) {
+                    const uint32_t mask = 0u - ((word >> j) & 1u);
+                    const uint32_t* row = m + i * 160 + j * 5;
+                    o[0] ^= row[0] & mask;
+                    o[1] ^= row[1] & mask;
+                    o[2] ^= row[2] & mask;
+                    o[3] ^= row[3] & mask;
+                    o[4] ^= row[4] & mask;
+                }
+            }
+            for (int w = 0; w < 5; w++) v[w] = o[w];
+        }
+    }
+    rt_rng_state* out = states + s;
+    out->d = st[0];
+    for (int i = 0; i < 5; i++) out->v[i] = v[i];
+    for (int i = 0; i < 6; i++) out->unused[i] = 0;
+}
+
+__global__ __launch_bounds__(BLOCK) void unshard_kernel(char* surface, uint64_t pitch, int width, int height,
+                                                        int shard_count, const float4* shards, int64_t per_shard,
+                                                        int tiles_x) {
+    const int rank = blockIdx.y;
+    const int64_t k = blockIdx.x;
+    const int tile = rank + (int)k * shard_count;
+    int lx, ly;
+    tile_pixel(threadIdx.x, &lx, &ly);
+    const int x = (tile % tiles_x) * TILE + lx, y = (tile / tiles_x) * TILE + ly;
+    if (tile >= tiles_x * ((height + TILE - 1) / TILE) || x >= width || y >= height) return;
+    const float4 v = shards[((size_t)rank * per_shard + k) * BLOCK + threadIdx.x];
+    *reinterpret_cast<float4*>(surface + (size_t)y * pitch + (size_t)x * 16) = v;
+}
+
+const uint32_t* device_jump_table() {
+    static std::mutex mu;
+    static std::map<int, uint32_t*> per_device;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = per_device.find(dev);
+    if (it != per_device.end()) return it->second;
+    uint32_t* d = nullptr;
+    const size_t bytes = (size_t)RT_XORWOW_JUMPS * 800 * 4;
+    if (hipMalloc(&d, bytes) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, rt_xorwow_jump_table(), bytes, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    per_device[dev] = d;
+    return d;
+}
+
+template <int STACK, bool STATS>
+hipError_t launch(const RenderArgs& args, int blocks, hipStream_t stream) {
+    hipLaunchKernelGGL((render_kernel<STACK, STATS>), dim3(blocks), dim3(BLOCK), 0, stream, args);
+    return hipGetLastError();
+}
+
+int tiles_of_shard(int width, int height, int shard_index, int shard_count) {
+    const int tiles = ((width + TILE - 1) / TILE) * ((height + TILE - 1) / TILE);
+    if (shard_index >= tiles) return 0;
+    return (tiles - shard_index + shard_count - 1) / shard_count;
+}
+
+// quat(vec3(0, PI, 0)) with PI = 3.1415926536f (main_raytracing.cu:7,151), glm
+// qua(eulerAngle) (type_quat.inl:204-213) using the RT deterministic sin/cos.
+void sky_quat(float* w, float* x, float* y, float* z) {
+    const float ex = 0.0f, ey = 3.1415926536f, ez = 0.0f;
+    const float cx = rtm::rt_cosf(ex * 0.5f), cy = rtm::rt_cosf(ey * 0.5f), cz = rtm::rt_cosf(ez * 0.5f);
+    const float sx = rtm::rt_sinf(ex * 0.5f), sy = rtm::rt_sinf(ey * 0.5f), sz = rtm::rt_sinf(ez * 0.5f);
+    *w = cx * cy * cz + sx * sy * sz;
+    *x = sx * cy * cz - cx * sy * sz;
+    *y = cx * sy * cz + sx * cy * sz;
+    *z = cx * cy * sz - sx * sy * cz;
+}
+
+}  // namespace
+
+extern "C" int64_t rt_shard_tiles(int width, int height, int shard_index, int shard_count) {
+    if (width <= 0 || height <= 0 || shard_count <= 0 || shard_index < 0 || shard_index >= shard_count) return 0;
+    return tiles_of_shard(width, height, shard_index, shard_count);
+}
+
+extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void* stream) {
+    if (!p || !scene) return set_error("rt_render: null argument");
+    if (p->width <= 0 || p->height <= 0 || p->spp <= 0 || p->bounces < 0)
+        return set_error("rt_render: bad frame size / spp / bounces");
+    if (p->shard_count <= 0 || p->shard_index < 0 || p->shard_index >= p->shard_count)
+        return set_error("rt_render: bad shard");
+    if (!p->out_shard && (!p->surface || p->pitch < (uint64_t)p->width * 16))
+        return set_error("rt_render: need a surface with pitch >= 16*width, or out_shard");
+    if (p->shard_count > 1 && !p->out_shard) return set_error("rt_render: sharded render needs out_shard");
+    if (!scene->rng_state || !scene->gpu_bvh_nodes || !scene->gpu_materials)
+        return set_error("rt_render: scene not uploaded (rng_state / bvh / materials missing)");
+    if ((p->flags & RT_RENDER_STATS) && !p->stats) return set_error("rt_render: stats flag without buffer");
+
+    RenderArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.spheres = scene->gpu_spheres;
+    a.materials = scene->gpu_materials;
+    a.nodes = scene->gpu_bvh_nodes;
+    a.face_indices = scene->gpu_bvh_face_indices;
+    a.vertices = scene->gpu_vertices;
+    a.faces = scene->gpu_faces;
+    a.rng = (rt_rng_state*)scene->rng_state;
+    a.sphere_count = scene->sphere_count;
+    a.cam = scene->camera;
+    if (scene->environment_cubemap_tex) {
+        const int n = cube_size(scene->environment_cubemap_tex);
+        if (n <= 0) return set_error("rt_render: unknown environment cube map handle");
+        a.sky = (const float*)scene->environment_cubemap_tex;
+        a.sky_n = n;
+    }
+    sky_quat(&a.qw, &a.qx, &a.qy, &a.qz);
+    a.surface = (char*)p->surface;
+    a.last = (const char*)p->surface_last_frame;
+    a.out_shard = (float4*)p->out_shard;
+    a.pitch = p->pitch;
+    a.width = p->width, a.height = p->height;
+    a.frame_index = p->frame_index, a.spp = p->spp, a.bounces = p->bounces;
+    a.shard_index = p->shard_index, a.shard_count = p->shard_count;
+    a.tiles_x = (p->width + TILE - 1) / TILE;
+    a.stats = (unsigned long long*)p->stats;
+    a.seg_counter = (unsigned long long*)p->segment_counter;
+
+    const int blocks = tiles_of_shard(p->width, p->height, p->shard_index, p->shard_count);
+    if (blocks == 0) return 0;
+    // Stack: the DFS holds at most depth+1 entries.  Depth is known when the scene was
+    // uploaded through rt_scene_upload; otherwise use the reference's 64 (main_raytracing.cu:35).
+    const int depth = rt_internal_lookup_depth(scene->gpu_bvh_nodes);
+    const bool small = depth >= 0 && depth + 2 <= 32;
+    const bool stats = (p->flags & RT_RENDER_STATS) != 0;
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e;
+    if (small)
+        e = stats ? launch<32, true>(a, blocks, s) : launch<32, false>(a, blocks, s);
+    else
+        e = stats ? launch<64, true>(a, blocks, s) : launch<64, false>(a, blocks, s);
+    return check(e, "render_kernel launch");
+}
+
+extern "C" int rt_init_rng(void* states, int width, int height, int shard_index, int shard_count, uint32_t seed,
+                           void* stream) {
+    if (!states || width <= 0 || height <= 0 || shard_count <= 0 || shard_index < 0 || shard_index >= shard_count)
+        return set_error("rt_init_rng: bad arguments");
+    const uint32_t* jump = device_jump_table();
+    if (!jump) return set_error("rt_init_rng: jump table upload failed");
+    const int tiles_x = (width + TILE - 1) / TILE;
+    int64_t count;
+    int sc;
+    if (shard_count == 1) {
+        count = (int64_t)width * height;
+        sc = 0;
+    } else {
+        count = (int64_t)tiles_of_shard(width, height, shard_index, shard_count) * BLOCK;
+        sc = shard_count;
+    }
+    if (count == 0) return 0;
+    const int blocks = (int)((count + BLOCK - 1) / BLOCK);
+    hipLaunchKernelGGL(init_rng_kernel, dim3(blocks), dim3(BLOCK), 0, (hipStream_t)stream, (rt_rng_state*)states, jump,
+                       seed, count, width, height, shard_index, sc, tiles_x);
+    return check(hipGetLastError(), "init_rng_kernel launch");
+}
+
+extern "C" int rt_unshard(void* surface, uint64_t pitch, int width, int height, int shard_count, const void* shards,
+                          int64_t per_shard, void* stream) {
+    if (!surface || !shards || shard_count <= 0 || per_shard <= 0) return set_error("rt_unshard: bad arguments");
+    const int tiles_x = (width + TILE - 1) / TILE;
+    hipLaunchKernelGGL(unshard_kernel, dim3((unsigned)per_shard, shard_count), dim3(BLOCK), 0, (hipStream_t)stream,
+                       (char*)surface, pitch, width, height, shard_count, (const float4*)shards, per_shard, tiles_x);
+    return check(hipGetLastError(), "unshard_kernel launch");
+}
+
+// ---------------------------------------------------------------------------------------
+// reference entry points
+// ---------------------------------------------------------------------------------------
+extern "C" void raytracing_process(void* surface, void* surface_last_frame, int width, int height, size_t pitch,
+                                   int frame_index, GPUScene* scene) {
+    rt_render_params p;
+    std::memset(&p, 0, sizeof(p));
+    p.surface = surface;
+    p.surface_last_frame = surface_last_frame;
+    p.width = width, p.height = height, p.pitch = pitch;
+    p.frame_index = frame_index;
+    p.spp = 5;      // main_raytracing.cu:166-170 (Release)
+    p.bounces = 6;  // main_raytracing.cu:115
+    p.shard_index = 0, p.shard_count = 1;
+    if (rt_render(&p, scene, nullptr) != 0)
+        std::printf("(raytracing_kernel_main) failed to launch error = %s\n", rt_last_error());
+}
+
+extern "C" void init_rng(uint32_t thread_block_count, uint32_t thread_block_size, void* states, unsigned int seed) {
+    const uint32_t* jump = device_jump_table();
+    const int64_t count = (int64_t)thread_block_count * thread_block_size;
+    if (!jump || count == 0) {
+        set_error("init_rng: jump table upload failed");
+        std::printf("(init_rng) failed: %s\n", rt_last_error());
+        return;
+    }
+    hipLaunchKernelGGL(init_rng_kernel, dim3(thread_block_count), dim3(thread_block_size), 0, nullptr,
+                       (rt_rng_state*)states, jump, seed, count, 0, 0, 0, 0, 0);
+    if (check(hipGetLastError(), "init_rng_kernel launch")) std::printf("(init_rng) failed: %s\n", rt_last_error());
+}

@@ -1,0 +1,271 @@
+/*
+ * rt_abi.h -- the C-ABI drop-in boundary of the MI355X ray tracer (librt_hip.so).
+ *
+ * Everything here is plain C: POD structs, raw pointers, sizes, integer status codes.
+ * No HIP, torch or C++ types appear in a signature, so the same header serves a C++ host
+ * (the reference's Scene.cpp / BVH.cpp / RayTracing.cpp), Python ctypes and any other FFI.
+ *
+ * Reference interfaces replaced (paths relative to the reference repository root):
+ *   raytracing_process ...... RayTracing/main_raytracing.cu:202-220 (declared by the caller
+ *                             at RayTracing/RayTracing.cpp:12)
+ *   init_rng ................ RayTracing/Random.cu:10-13 (caller RayTracing/RayTracing.cpp:13,220)
+ *   rt_malloc / rt_free ..... CUDA::DeviceMemory, utils/CUDAHelper.h:114-156
+ *   rt_memcpy_* ............. CUDA_CHECK(cudaMemcpy(...)) at RayTracing/Scene.cpp:195-230 and
+ *                             RayTracing/RayTracing.cpp:233
+ *   rt_cubemap_* ............ CUDA::Texture + Loader::LoadDDSFromFile,
+ *                             utils/CUDATexture.cpp:112-172,187-249
+ *   GPU data contract ....... RayTracing/GPUScene.h:11-96, RayTracing/Math.h:25-37
+ *
+ * Error behaviour: every rt_* function returns 0 on success and a nonzero code on
+ * failure, with a message available from rt_last_error().  The two reference entry points
+ * keep the reference's void signature; like main_raytracing.cu:215-219 they print a launch
+ * failure, and additionally record it for rt_last_error().
+ */
+#ifndef RT_ABI_H
+#define RT_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__cplusplus)
+#define RT_ALIGNAS(n) alignas(n)
+#else
+#define RT_ALIGNAS(n) _Alignas(n)
+#endif
+
+/* ---------------------------------------------------------------------------------------
+ * Data contract.  Field order, sizes and alignment are those of the reference structs
+ * (GPUScene.h), so buffers built by the reference's Scene::Upload are consumed unchanged.
+ * ------------------------------------------------------------------------------------- */
+
+/* GPUScene.h:11-23.  60 bytes. */
+typedef struct GPUCamera {
+    float origin[3];
+    float viewport_worldspace_size[2];
+    float aspect;
+    float horizontal[3];
+    float vertical[3];
+    float lower_left_corner[3];
+} GPUCamera;
+
+/* GPUScene.h:25-30.  32 bytes. */
+typedef struct GPUVertex {
+    RT_ALIGNAS(16) float position[3];
+    float normal[3];
+    float uv[2];
+} GPUVertex;
+
+/* GPUScene.h:32-38.  16 bytes.  NOTE the reference's field order v0, v2, v1: the aggregate
+ * initialiser GPUFace{i0, i0+1, i0+2} in Scene::AddTriangle (Scene.cpp:65) therefore lands
+ * as v0=i0, v2=i0+1, v1=i0+2, and the kernel reads v1/v2 by name. */
+typedef struct GPUFace {
+    RT_ALIGNAS(16) uint32_t v0;
+    uint32_t v2;
+    uint32_t v1;
+    uint32_t material;
+} GPUFace;
+
+/* GPUScene.h:40-50 + Math.h:25-37 (AABB).  32 bytes.  Leaf iff prim_count > 0; an inner
+ * node's children are at first_index and first_index + 1. */
+typedef struct GPUBVHNode {
+    RT_ALIGNAS(32) float bmin[3];
+    float bmax[3];
+    uint32_t first_index;
+    uint32_t prim_count;
+} GPUBVHNode;
+
+/* GPUScene.h:59-64.  32 bytes. */
+typedef struct GeometrySphere {
+    RT_ALIGNAS(16) float position[3];
+    float radius;
+    int32_t material;
+} GeometrySphere;
+
+/* GPUScene.h:66-74.  64 bytes. */
+typedef struct GPUMaterial {
+    RT_ALIGNAS(16) float albedo[4];
+    float emissive[4];
+    float specular[4];
+    float roughness;
+    float specular_percent;
+    float IOR;
+} GPUMaterial;
+
+/* GPUScene.h:76-96.  136 bytes.  All pointers are non-owning device pointers.
+ * rng_state points at a caller-owned array of rt_rng_state (48 B each, the size of the
+ * reference's curandState), one per pixel, indexed y*width + x (GPUScene.h:95).
+ * environment_cubemap_tex is a handle from rt_cubemap_create (0 = black sky). */
+typedef struct GPUScene {
+    const GeometrySphere* gpu_spheres;
+    const GPUMaterial* gpu_materials;
+    const GPUBVHNode* gpu_bvh_nodes;
+    const uint32_t* gpu_bvh_face_indices;
+    const GPUVertex* gpu_vertices;
+    const GPUFace* gpu_faces;
+    int32_t sphere_count;
+    int32_t material_count;
+    void* rng_state;
+    uint64_t environment_cubemap_tex;
+    GPUCamera camera;
+} GPUScene;
+
+/* Per-pixel XORWOW state.  Same size and the same first 24 bytes as the reference's
+ * curandStateXORWOW (d, v[5]); the Box-Muller fields are never used by this path. */
+typedef struct rt_rng_state {
+    RT_ALIGNAS(8) uint32_t d;
+    uint32_t v[5];
+    uint32_t unused[6];
+} rt_rng_state;
+
+#if defined(__cplusplus)
+static_assert(sizeof(GPUCamera) == 60, "GPUCamera");
+static_assert(sizeof(GPUVertex) == 32, "GPUVertex");
+static_assert(sizeof(GPUFace) == 16 && offsetof(GPUFace, v2) == 4 && offsetof(GPUFace, v1) == 8, "GPUFace");
+static_assert(sizeof(GPUBVHNode) == 32 && offsetof(GPUBVHNode, first_index) == 24, "GPUBVHNode");
+static_assert(sizeof(GeometrySphere) == 32, "GeometrySphere");
+static_assert(sizeof(GPUMaterial) == 64 && offsetof(GPUMaterial, roughness) == 48, "GPUMaterial");
+static_assert(sizeof(GPUScene) == 136 && offsetof(GPUScene, sphere_count) == 48 &&
+              offsetof(GPUScene, rng_state) == 56 && offsetof(GPUScene, environment_cubemap_tex) == 64 &&
+              offsetof(GPUScene, camera) == 72, "GPUScene");
+static_assert(sizeof(rt_rng_state) == 48, "rt_rng_state");
+#endif
+
+/* ---------------------------------------------------------------------------------------
+ * Reference entry points (exact signatures).
+ * ------------------------------------------------------------------------------------- */
+
+/* main_raytracing.cu:202.  Renders one progressive frame into the pitched float4 surface:
+ * reference constants sample_count = 5 (main_raytracing.cu:166-170, Release) and
+ * num_bounces = 6 (:115), on the null stream, asynchronous. */
+void raytracing_process(void* surface, void* surface_last_frame, int width, int height, size_t pitch,
+                        int frame_index, GPUScene* scene);
+
+/* Random.cu:10.  curand_init(seed, tid, 0) for tid in [0, count*size): XORWOW seeding
+ * plus a skip-ahead of tid * 2^67 draws.  Null stream, asynchronous. */
+void init_rng(uint32_t thread_block_count, uint32_t thread_block_size, void* rngStates, unsigned int seed);
+
+/* ---------------------------------------------------------------------------------------
+ * Extended entry points (runtime parameters the reference hard-codes, streams, shards).
+ * ------------------------------------------------------------------------------------- */
+
+typedef struct rt_render_params {
+    void* surface;                 /* pitched float4 output (or NULL when out_shard is set) */
+    const void* surface_last_frame;/* pitched float4 history, same pitch */
+    int32_t width, height;
+    uint64_t pitch;                /* bytes per row of both surfaces */
+    int32_t frame_index;
+    int32_t spp;                   /* reference: 5 (Release) / 1 (Debug) */
+    int32_t bounces;               /* reference: 6 */
+    int32_t shard_index;           /* tile sharding: this rank renders 16x16 tiles */
+    int32_t shard_count;           /*   t = shard_index + k * shard_count (row-major tiles) */
+    int32_t flags;                 /* RT_RENDER_* */
+    void* out_shard;               /* if non-NULL: compact [k][16*16] float4 shard output */
+    uint64_t* stats;               /* RT_RENDER_STATS: RT_STAT_COUNT uint64 counters (zeroed by caller) */
+    uint64_t* segment_counter;     /* optional: += ray segments traced (GetRayHit calls) */
+} rt_render_params;
+
+#define RT_RENDER_STATS 1          /* count traversal work (slower kernel variant) */
+
+enum {
+    RT_STAT_SEGMENTS = 0,   /* GetRayHit calls */
+    RT_STAT_NODES = 1,      /* BVH nodes popped (AABB tests) */
+    RT_STAT_TRI_TESTS = 2,  /* ray/triangle tests */
+    RT_STAT_TRI_ACCEPTS = 3,/* triangle hits accepted as the new closest */
+    RT_STAT_SPHERE_ACCEPTS = 4,
+    RT_STAT_HITS = 5,       /* segments that hit something */
+    RT_STAT_MISSES = 6,     /* segments that sampled the sky */
+    RT_STAT_COUNT = 8
+};
+
+/* Render on `stream` (a hipStream_t, NULL = null stream).  Returns 0 or an error code. */
+int rt_render(const rt_render_params* params, const GPUScene* scene, void* stream);
+
+/* init_rng for the pixels of one shard: state index s of shard (shard_index, shard_count)
+ * of a width x height frame gets curand_init(seed, pixel_id(s), 0).  With shard_count == 1
+ * the states are in y*width + x order (reference layout); otherwise they are compact in the
+ * shard's tile order.  Returns 0 or an error code. */
+int rt_init_rng(void* rng_states, int width, int height, int shard_index, int shard_count, uint32_t seed,
+                void* stream);
+
+/* Number of pixels of a shard (tiles of 16x16, partial edge tiles counted as rendered
+ * pixels of the tile: the compact shard always holds whole tiles). */
+int64_t rt_shard_tiles(int width, int height, int shard_index, int shard_count);
+
+/* Un-permute gathered compact shards [shard_count][tiles_per_shard_max][256] float4 into a
+ * pitched surface.  Returns 0 or an error code. */
+int rt_unshard(void* surface, uint64_t pitch, int width, int height, int shard_count, const void* shards,
+               int64_t tiles_per_shard_max, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Device memory / texture shim (replaces utils/CUDAHelper.h and utils/CUDATexture.*).
+ * ------------------------------------------------------------------------------------- */
+int rt_set_device(int device);
+int rt_malloc(void** ptr, size_t bytes);
+int rt_malloc_pitch(void** ptr, size_t* pitch, size_t width_bytes, size_t height);
+int rt_free(void* ptr);
+int rt_memcpy_h2d(void* dst, const void* src, size_t bytes);
+int rt_memcpy_d2h(void* dst, const void* src, size_t bytes);
+int rt_memcpy_d2d(void* dst, const void* src, size_t bytes);
+int rt_memset(void* dst, int value, size_t bytes);
+int rt_synchronize(void);
+const char* rt_last_error(void);
+
+/* Cube map from level-0 fp32 RGBA faces [6][size][size][4] (host memory), face order
+ * +X,-X,+Y,-Y,+Z,-Z.  Sampled in software (bilinear, seamless).  Returns 0 on failure. */
+uint64_t rt_cubemap_create(const float* rgba_level0, int size);
+int rt_cubemap_destroy(uint64_t handle);
+
+/* ---------------------------------------------------------------------------------------
+ * Host scene (C++ mirror of RayTracing::Scene / BVH / Camera, RayTracing/Scene.{h,cpp},
+ * RayTracing/BVH.{h,cpp}) exposed for non-C++ hosts.  rt_scene is opaque.
+ * ------------------------------------------------------------------------------------- */
+typedef struct rt_scene rt_scene;
+
+rt_scene* rt_scene_create(void);
+void rt_scene_destroy(rt_scene* scene);
+uint32_t rt_scene_add_material(rt_scene* scene, const GPUMaterial* material);
+void rt_scene_add_triangle(rt_scene* scene, const float a[3], const float b[3], const float c[3], int material);
+void rt_scene_add_quad(rt_scene* scene, const float a[3], const float b[3], const float c[3], const float d[3],
+                       int material);
+void rt_scene_add_sphere(rt_scene* scene, const float position[3], float radius, int material);
+/* Scene::AddLoadedScene with a mesh asset (assets/bunny_mesh.bin format) and a column-major
+ * 4x4 transform.  Returns 0 or an error code. */
+int rt_scene_add_mesh_file(rt_scene* scene, const char* path, const float transform[16], int material);
+/* Environment cube map from an asset (assets/sunset_cube128.bin) or a legacy fp32 DDS. */
+int rt_scene_set_environment_file(rt_scene* scene, const char* path);
+void rt_scene_set_camera(rt_scene* scene, const float position[3], float angle_x_deg, float angle_y_deg);
+void rt_scene_set_viewport(rt_scene* scene, int width, int height);
+/* Scene::Upload: builds the BVH when dirty, uploads dirty buffers, fills the GPUScene. */
+int rt_scene_upload(rt_scene* scene, void* rng_state);
+const GPUScene* rt_scene_gpu(const rt_scene* scene);
+/* The host half of Scene::Upload without any device work: camera basis + BVH build. */
+void rt_scene_build(rt_scene* scene);
+/* The camera basis as of the last build/upload. */
+void rt_scene_camera(const rt_scene* scene, GPUCamera* out);
+/* CUDARayTracer::SetupCornellBox + SetupStanfordBunny (RayTracing.cpp:79-203, 33-69);
+ * which = 0: Cornell box + bunny (configs 1-3), 1: 4x bunny (config 4), 2: 1M-tri plane
+ * (config 5). */
+int rt_scene_setup(rt_scene* scene, int which, const char* assets_dir);
+/* Config-5 scene with an n x n quad grid (n = 708 for the benchmark). */
+int rt_scene_setup_plane(rt_scene* scene, int n, const char* assets_dir);
+/* Host views of the scene arrays (valid until the next modification). */
+size_t rt_scene_host_arrays(const rt_scene* scene, const GPUBVHNode** nodes, size_t* node_count,
+                            const uint32_t** face_indices, size_t* face_count, const GPUVertex** vertices,
+                            size_t* vertex_count, const GPUFace** faces);
+int rt_scene_bvh_max_depth(const rt_scene* scene);
+
+/* XORWOW jump matrix A^(4^k * 2^67) (k < 32) as 800 uint32 words in rocrand's layout
+ * m[i*160 + j*5 + w] (input word i, bit j, output word w).  For tests. */
+int rt_xorwow_jump_matrix(int k, uint32_t out[800]);
+/* Host-side curand_init(seed, subsequence, 0) for tests. */
+void rt_xorwow_init_host(uint32_t seed, uint64_t subsequence, rt_rng_state* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_ABI_H */

@@ -1,0 +1,118 @@
+"""Test helpers: load the product package and the CPU oracle (oracle/liboracle.so).
+
+The oracle is test infrastructure (see oracle/rt_oracle.c header): it is loaded only here,
+by __graft_entry__.smoke() and by bench.py's cpu_baseline leg.
+"""
+import ctypes
+import importlib.util
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ASSETS = os.path.join(ROOT, "assets")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+ORACLE_LIB = os.path.join(ROOT, "oracle", "liboracle.so")
+SEED = 0xDEADBEEF
+
+
+def load_rt():
+    if "cuda_raytracing_amd" in sys.modules:
+        return sys.modules["cuda_raytracing_amd"]
+    spec = importlib.util.spec_from_file_location(
+        "cuda_raytracing_amd", os.path.join(ROOT, "cuda-raytracing_amd", "__init__.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["cuda_raytracing_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+_P, _SZ, _I, _U32, _U64, _F = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float
+_oracle = None
+
+
+def oracle():
+    global _oracle
+    if _oracle is None:
+        if not os.path.exists(ORACLE_LIB):
+            raise RuntimeError("oracle/liboracle.so not built (run __graft_entry__.build())")
+        L = ctypes.CDLL(ORACLE_LIB)
+        L.oracle_scene_create.restype = _P
+        L.oracle_scene_create.argtypes = [_I, ctypes.c_char_p, _I]
+        L.oracle_scene_destroy.argtypes = [_P]
+        L.oracle_scene_arrays.argtypes = [_P] + [ctypes.POINTER(t) for t in (_P, _SZ, _P, _SZ, _P, _SZ, _P, _I, _P, _I, _P, _I)]
+        L.oracle_camera.argtypes = [_P, _I, _I, ctypes.POINTER(_F)]
+        L.oracle_set_camera.argtypes = [_P, ctypes.POINTER(_F), _F, _F]
+        L.oracle_rng_init.argtypes = [_U32, _U64, ctypes.POINTER(_U32)]
+        L.oracle_rng_init_frame.argtypes = [_U32, _I, _I, _P, _I]
+        L.oracle_rng_draws.argtypes = [ctypes.POINTER(_U32), _I, ctypes.POINTER(_F)]
+        L.oracle_jump_matrix.argtypes = [_I, ctypes.POINTER(_U32)]
+        L.oracle_jump_matrix.restype = _I
+        L.oracle_sin.argtypes = L.oracle_cos.argtypes = [_F]
+        L.oracle_sin.restype = L.oracle_cos.restype = _F
+        L.oracle_render.restype = _I
+        L.oracle_render.argtypes = [_P, _I, _I, _I, _I, _I, _U32, _P, _P, _P, _I, _I, _I, _P]
+        _oracle = L
+    return _oracle
+
+
+class OracleScene:
+    WHICH = {"bunny": 0, "bunny4": 1, "plane1m": 2}
+
+    def __init__(self, which="bunny", grid_n=708):
+        self.h = oracle().oracle_scene_create(self.WHICH[which], ASSETS.encode(), grid_n)
+        if not self.h:
+            raise RuntimeError("oracle_scene_create failed")
+
+    def __del__(self):
+        if getattr(self, "h", None) and _oracle is not None:
+            _oracle.oracle_scene_destroy(self.h)
+
+    def arrays(self):
+        v = [_P(), _SZ(), _P(), _SZ(), _P(), _SZ(), _P(), _I(), _P(), _I(), _P(), _I()]
+        oracle().oracle_scene_arrays(self.h, *[ctypes.byref(x) for x in v])
+        grab = lambda p, n: np.frombuffer(ctypes.string_at(p.value, n), dtype=np.uint8).copy() if n else np.zeros(0, np.uint8)
+        return {"vertices": grab(v[0], v[1].value * 32), "faces": grab(v[2], v[3].value * 16),
+                "nodes": grab(v[4], v[5].value * 32), "face_indices": grab(v[6], v[3].value * 4),
+                "max_depth": v[7].value, "spheres": grab(v[8], v[9].value * 32), "materials": grab(v[10], v[11].value * 64)}
+
+    def camera(self, w, h):
+        out = (ctypes.c_float * 15)()
+        oracle().oracle_camera(self.h, w, h, out)
+        return np.array(out[:], dtype=np.float32)
+
+    def render(self, w, h, spp, bounces, frame_index=0, seed=SEED, rng=None, last=None, rows=None, threads=0,
+               stats=False):
+        r0, r1 = rows if rows else (0, h)
+        out = np.zeros((r1 - r0, w, 4), dtype=np.float32)
+        st = np.zeros(8, dtype=np.uint64)
+        rp = rng.ctypes.data if rng is not None else None
+        lp = np.ascontiguousarray(last, dtype=np.float32).ctypes.data if last is not None else None
+        keep = last
+        code = oracle().oracle_render(self.h, w, h, spp, bounces, frame_index, seed, rp, lp, out.ctypes.data, r0, r1,
+                                      threads, st.ctypes.data)
+        del keep
+        assert code == 0
+        return (out, st) if stats else out
+
+
+def oracle_rng_state(seed, sub):
+    out = (ctypes.c_uint32 * 6)()
+    oracle().oracle_rng_init(seed, sub, out)
+    return np.array(out[:], dtype=np.uint32)
+
+
+def oracle_rng_frame(seed, w, h, threads=0):
+    out = np.zeros((h * w, 6), dtype=np.uint32)
+    oracle().oracle_rng_init_frame(seed, w, h, out.ctypes.data, threads)
+    return out
+
+
+def product_scene(which="bunny", w=64, h=36):
+    rt = load_rt()
+    s = rt.Scene()
+    s.setup(which)
+    s.set_viewport(w, h)
+    s.build()
+    return s

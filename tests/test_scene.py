@@ -1,0 +1,79 @@
+"""Product host code (C++ Scene/BVH/Camera mirror) against the independent C oracle:
+byte-identical scene arrays, BVH and camera basis.  No GPU work."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import rt_testlib as T
+
+GOLD = json.load(open(os.path.join(T.GOLDEN, "golden.json")))
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("which", ["bunny", "bunny4"])
+def test_scene_arrays_match_oracle(which):
+    p = T.product_scene(which).host_arrays()
+    o = T.OracleScene(which).arrays()
+    for k in ("vertices", "faces", "nodes", "face_indices"):
+        assert p[k].shape == o[k].shape and np.array_equal(p[k], o[k]), k
+
+
+def test_bunny4_counts():
+    g = GOLD["bunny4_scene"]
+    assert g["faces"] == 555622  # 277,804 geometric triangles x2 + 14
+    p = T.product_scene("bunny4").host_arrays()
+    assert sha(p["nodes"]) == g["nodes_sha256"] and sha(p["face_indices"]) == g["face_indices_sha256"]
+
+
+def test_plane_grid_matches_oracle():
+    rt = T.load_rt()
+    s = rt.Scene()
+    s.setup_plane(40)
+    s.set_viewport(64, 36)
+    s.build()
+    p = s.host_arrays()
+    o = T.OracleScene("plane1m", grid_n=40).arrays()
+    assert len(p["faces"]) // 16 == 2 * 40 * 40
+    for k in ("vertices", "faces", "nodes", "face_indices"):
+        assert np.array_equal(p[k], o[k]), k
+
+
+@pytest.mark.parametrize("w,h,ax,ay,pos", [(1920, 1080, 0, 180, (0, 0, 0)), (256, 256, 0, 180, (0, 0, 0)),
+                                           (61, 37, 12.5, -33.0, (1.5, -2.0, 3.25))])
+def test_camera_matches_oracle(w, h, ax, ay, pos):
+    rt = T.load_rt()
+    s = rt.Scene()
+    s.setup("bunny")
+    s.set_camera(pos, ax, ay)
+    s.set_viewport(w, h)
+    s.build()
+    cam = np.frombuffer(bytes(s.camera()), dtype=np.float32)
+    o = T.OracleScene("bunny")
+    import ctypes
+    o_pos = (ctypes.c_float * 3)(*pos)
+    T.oracle().oracle_set_camera(o.h, o_pos, ax, ay)
+    assert np.array_equal(cam, o.camera(w, h))
+    if (w, h, ax, ay) == (1920, 1080, 0, 180):
+        assert [float(x) for x in cam] == GOLD["camera_1920x1080"]
+
+
+def test_bvh_invariants():
+    s = T.product_scene("bunny")
+    a = s.host_arrays()
+    nodes = a["nodes"].view(np.float32).reshape(-1, 8)
+    ints = a["nodes"].view(np.uint32).reshape(-1, 8)
+    first, count = ints[:, 6], ints[:, 7]
+    fi = a["face_indices"].view(np.uint32)
+    assert np.array_equal(np.sort(fi), np.arange(len(fi), dtype=np.uint32))  # a permutation
+    leaves = count > 0
+    assert count[leaves].sum() == len(fi)
+    inner = np.where(~leaves)[0]
+    for c in (first[inner], first[inner] + 1):  # children inside the parent box
+        assert (nodes[c, :3] >= nodes[inner, :3]).all() and (nodes[c, 3:6] <= nodes[inner, 3:6]).all()
+    assert s.max_depth() == 25
