@@ -308,6 +308,7 @@ void Scene::BuildHost() {
 
 // Scene.cpp:182-234
 void Scene::Upload(void* rng) {
+    BuildHost();  // camera.Update() + BVH::Calculate when dirty
     static_cast<GPUScene*>(this)->camera = static_cast<const GPUCamera&>(camera);
     rng_state = rng;
     if (environment_dirty) {
@@ -318,7 +319,6 @@ void Scene::Upload(void* rng) {
     }
     environment_cubemap_tex = environment;
 
-    BuildHost();
     if (bvh_upload_pending) {
         bvh_upload_pending = false;
         const size_t nb = bvh->GetNodeCount() * sizeof(GPUBVHNode);
