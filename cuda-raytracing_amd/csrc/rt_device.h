@@ -22,12 +22,11 @@ RT_HD bool intersect_aabb(f3 o, f3 d, const float* bmin, const float* bmax, floa
     return tmax >= tmin && tmin < ray_length && tmax > 0;
 }
 
-// glm::intersectRayTriangle (include/glm/gtx/intersect.inl:29-94); `dir` is normalized.
+// glm::intersectRayTriangle (include/glm/gtx/intersect.inl:29-94) with the two edges
+// edge1 = vert1 - vert0, edge2 = vert2 - vert0 already formed; `dir` is normalized.
 // On success writes bary (scaled by 1/det) and distance.
-RT_HD bool intersect_triangle(f3 orig, f3 dir, f3 v0, f3 v1, f3 v2, float* bx, float* by, float* distance) {
+RT_HD bool intersect_triangle_e(f3 orig, f3 dir, f3 v0, f3 edge1, f3 edge2, float* bx, float* by, float* distance) {
     const float eps = 1.1920928955078125e-07f;  // std::numeric_limits<float>::epsilon()
-    const f3 edge1 = rtm::sub(v1, v0);
-    const f3 edge2 = rtm::sub(v2, v0);
     const f3 p = rtm::cross(dir, edge2);
     const float det = rtm::dot(edge1, p);
     f3 perp;
@@ -54,6 +53,10 @@ RT_HD bool intersect_triangle(f3 orig, f3 dir, f3 v0, f3 v1, f3 v2, float* bx, f
     *bx = u * inv_det;
     *by = v * inv_det;
     return true;
+}
+
+RT_HD bool intersect_triangle(f3 orig, f3 dir, f3 v0, f3 v1, f3 v2, float* bx, float* by, float* distance) {
+    return intersect_triangle_e(orig, dir, v0, rtm::sub(v1, v0), rtm::sub(v2, v0), bx, by, distance);
 }
 
 // glm::intersectRaySphere (intersect.inl:135-153) with the squared radius.

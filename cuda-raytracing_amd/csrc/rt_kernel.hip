@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -25,7 +26,7 @@
 #include "rt_math.h"
 #include "xorwow.h"
 
-int rt_internal_lookup_depth(const void* gpu_nodes);
+bool rt_internal_lookup_mirror(const GPUScene* scene, const void** tris, int* depth);
 
 // ---------------------------------------------------------------------------------------
 // error state
@@ -102,8 +103,17 @@ static int cube_size(uint64_t handle) {
 // ---------------------------------------------------------------------------------------
 namespace {
 
-constexpr int TILE = 16;
-constexpr int BLOCK = 256;
+constexpr int TILE = 16;   // shard / tile granularity (16x16 pixels)
+constexpr int BLOCK = 256; // threads of the tile-shaped helper kernels
+constexpr int WAVE = 64;
+
+// Leaf-ordered triangle record (product-side mirror of the reference arrays, built by
+// Scene::Upload): A = (v0.xyz, e1.x), B = (e1.yz, e2.xy), C = (e2.z, face id, 0, 0) with
+// e1 = v1 - v0 and e2 = v2 - v0 computed exactly as glm::intersectRayTriangle does
+// (gtx/intersect.inl:37-38), so the test below is bit-identical to the reference's.
+struct FlatTri {
+    float4 a, b, c;
+};
 
 struct RenderArgs {
     const GeometrySphere* spheres;
@@ -112,6 +122,7 @@ struct RenderArgs {
     const uint32_t* face_indices;
     const GPUVertex* vertices;
     const GPUFace* faces;
+    const FlatTri* tris;  // null -> reference-layout tracer
     rt_rng_state* rng;
     const float* sky;  // float4 [6][n][n] or null
     int sky_n;
@@ -128,33 +139,189 @@ struct RenderArgs {
     unsigned long long* seg_counter;
 };
 
+struct Counters {
+    unsigned long long seg = 0, node = 0, tri = 0, tacc = 0, sacc = 0, hit = 0, miss = 0;
+};
+
+struct Hit {
+    float best;
+    int kind;  // 0 none, 1 sphere, 2 triangle
+    uint32_t id;  // sphere index or face index
+    float bx, by;
+};
+
 __device__ __forceinline__ rtm::f3 ld3(const float* p) { return rtm::f3{p[0], p[1], p[2]}; }
 
-// Tile-local pixel of thread `tid`: wave w covers the 8x8 sub-tile ((w&1)*8, (w>>1)*8).
+// Tile-local pixel of tile-thread `tid` (0..255): wave w covers the 8x8 sub-tile
+// ((w&1)*8, (w>>1)*8), lane l the pixel (l&7, l>>3) of it.  The compact shard layout and
+// unshard_kernel use the same map.
 __device__ __forceinline__ void tile_pixel(int tid, int* lx, int* ly) {
     const int w = tid >> 6, l = tid & 63;
     *lx = (w & 1) * 8 + (l & 7);
     *ly = (w >> 1) * 8 + (l >> 3);
 }
 
-template <int STACK, bool STATS>
-__global__ __launch_bounds__(BLOCK) void render_kernel(RenderArgs a) {
-    __shared__ uint32_t stack_lds[STACK * BLOCK];
-    uint32_t* const stk = stack_lds + threadIdx.x;
+// The sphere loop of GetRayHit (main_raytracing.cu:88-103): strict `<` replaces.
+template <bool STATS>
+__device__ __forceinline__ void trace_spheres(const RenderArgs& a, rtm::f3 ro, rtm::f3 nd, Hit& h, Counters& c) {
+    for (int i = 0; i < a.sphere_count; i++) {
+        const GeometrySphere& sp = a.spheres[i];
+        float dist;
+        if (rtd::intersect_sphere(ro, nd, ld3(sp.position), sp.radius * sp.radius, &dist)) {
+            if (dist >= h.best) continue;
+            h.best = dist;
+            h.kind = 1;
+            h.id = (uint32_t)i;
+            if (STATS) c.sacc++;
+        }
+    }
+}
 
-    const int tile = a.shard_index + (int)blockIdx.x * a.shard_count;
-    int lx, ly;
-    tile_pixel(threadIdx.x, &lx, &ly);
-    const int x = (tile % a.tiles_x) * TILE + lx;
-    const int y = (tile / a.tiles_x) * TILE + ly;
-    unsigned long long n_seg = 0, n_node = 0, n_tri = 0, n_tacc = 0, n_sacc = 0, n_hit = 0, n_miss = 0;
-    // Off-frame lanes of edge tiles skip the work but stay for the wave reduction below.
-    if (x < a.width && y < a.height) {
-    const size_t rng_index =
-        a.shard_count == 1 ? (size_t)y * a.width + x : (size_t)blockIdx.x * BLOCK + threadIdx.x;
+// BVHRayHit (main_raytracing.cu:33-81) on the reference arrays, literally: uint32 stack,
+// pop, AABB test against the current closest distance, leaf -> face_indices -> faces ->
+// vertices, inner -> push first, first+1 (right child popped first).  Used for scenes
+// whose buffers were not uploaded through rt_scene_upload (no leaf-ordered mirror).
+struct RefTracer {
+    static constexpr int WORDS = 1;
+    template <int STACK, bool STATS>
+    __device__ static void trace(const RenderArgs& a, uint32_t* stk, rtm::f3 ro, rtm::f3 rd, rtm::f3 nd, Hit& h,
+                                 Counters& c) {
+        int sp = 0;
+        stk[0] = 0u;
+        sp = 1;
+        while (sp) {
+            const GPUBVHNode& node = a.nodes[stk[(--sp) * WAVE]];
+            if (STATS) c.node++;
+            if (!rtd::intersect_aabb(ro, rd, node.bmin, node.bmax, h.best)) continue;
+            if (node.prim_count > 0) {
+                for (uint32_t i = 0; i < node.prim_count; i++) {
+                    const uint32_t fi = a.face_indices[node.first_index + i];
+                    const GPUFace f = a.faces[fi];
+                    float bx, by, dist;
+                    if (STATS) c.tri++;
+                    if (rtd::intersect_triangle(ro, nd, ld3(a.vertices[f.v0].position), ld3(a.vertices[f.v1].position),
+                                                ld3(a.vertices[f.v2].position), &bx, &by, &dist)) {
+                        if (dist >= h.best || dist < 0.0f) continue;
+                        h.best = dist;
+                        h.kind = 2;
+                        h.id = fi;
+                        h.bx = bx;
+                        h.by = by;
+                        if (STATS) c.tacc++;
+                    }
+                }
+            } else {
+                stk[(sp++) * WAVE] = node.first_index;
+                stk[(sp++) * WAVE] = node.first_index + 1;
+            }
+        }
+    }
+};
+
+// The slab part of IntersectAABB (Math.h:50-61) that does not depend on the closest
+// distance: returns tmin and whether tmax >= tmin && tmax > 0.  The remaining clause,
+// tmin < ray_length, is evaluated when the reference would pop the node.
+__device__ __forceinline__ bool slab(rtm::f3 o, rtm::f3 d, float4 lo, float4 hi, float* tmin_out) {
+    // lo = (bmin.x, bmin.y, bmin.z, bmax.x), hi = (bmax.y, bmax.z, first, count)
+    float tx1 = (lo.x - o.x) / d.x, tx2 = (lo.w - o.x) / d.x;
+    float tmin = fminf(tx1, tx2), tmax = fmaxf(tx1, tx2);
+    float ty1 = (lo.y - o.y) / d.y, ty2 = (hi.x - o.y) / d.y;
+    tmin = fmaxf(tmin, fminf(ty1, ty2)), tmax = fminf(tmax, fmaxf(ty1, ty2));
+    float tz1 = (lo.z - o.z) / d.z, tz2 = (hi.y - o.z) / d.z;
+    tmin = fmaxf(tmin, fminf(tz1, tz2)), tmax = fminf(tmax, fmaxf(tz1, tz2));
+    *tmin_out = tmin;
+    return tmax >= tmin && tmax > 0;
+}
+
+// The same traversal, re-associated for the GPU without changing a single decision:
+//  * siblings are adjacent (children of an inner node at first, first+1), so an inner node
+//    loads both children (64 contiguous bytes) and runs both slab tests at once; the right
+//    child -- the one the reference pops next -- continues in registers, the left child is
+//    pushed with its tmin, and `tmin < closest` is checked when it is popped, against the
+//    closest distance at that moment, exactly as the reference's pop-time test;
+//  * leaves read the leaf-ordered FlatTri mirror (one 48-byte record per test instead of
+//    the index -> face -> 3 vertex dependent-load chain);
+//  * node visit order, tested triangles and their order, and every comparison are the
+//    reference's, so the closest hit (including ties between coincident faces) is identical.
+// Stack entries: (node index, tmin bits) in LDS, [entry][lane].
+struct FlatTracer {
+    static constexpr int WORDS = 2;
+    template <int STACK, bool STATS>
+    __device__ static void trace(const RenderArgs& a, uint32_t* stk, rtm::f3 ro, rtm::f3 rd, rtm::f3 nd, Hit& h,
+                                 Counters& c) {
+        const float4* nodes4 = reinterpret_cast<const float4*>(a.nodes);
+        // root (node 0), tested against the closest sphere distance
+        float4 lo = nodes4[0], hi = nodes4[1];
+        float tmin;
+        if (STATS) c.node++;
+        if (!slab(ro, rd, lo, hi, &tmin) || !(tmin < h.best)) return;
+        uint32_t first = __float_as_uint(hi.z), count = __float_as_uint(hi.w);
+        int sp = 0;
+        for (;;) {
+            if (count > 0) {
+                // leaf: the reference's per-triangle loop over face_indices[first .. first+count)
+                for (uint32_t i = first; i < first + count; i++) {
+                    const FlatTri t = a.tris[i];
+                    if (STATS) c.tri++;
+                    const rtm::f3 v0 = rtm::mk(t.a.x, t.a.y, t.a.z);
+                    const rtm::f3 e1 = rtm::mk(t.a.w, t.b.x, t.b.y);
+                    const rtm::f3 e2 = rtm::mk(t.b.z, t.b.w, t.c.x);
+                    float bx, by, dist;
+                    if (rtd::intersect_triangle_e(ro, nd, v0, e1, e2, &bx, &by, &dist)) {
+                        if (dist >= h.best || dist < 0.0f) continue;
+                        h.best = dist;
+                        h.kind = 2;
+                        h.id = __float_as_uint(t.c.y);
+                        h.bx = bx;
+                        h.by = by;
+                        if (STATS) c.tacc++;
+                    }
+                }
+            } else {
+                const float4 l0 = nodes4[2 * first], l1 = nodes4[2 * first + 1];
+                const float4 r0 = nodes4[2 * first + 2], r1 = nodes4[2 * first + 3];
+                if (STATS) c.node += 2;
+                float tl, tr;
+                const bool okl = slab(ro, rd, l0, l1, &tl);
+                const bool okr = slab(ro, rd, r0, r1, &tr);
+                if (okr && tr < h.best) {
+                    if (okl) {
+                        stk[(sp * 2) * WAVE] = first;
+                        stk[(sp * 2 + 1) * WAVE] = __float_as_uint(tl);
+                        sp++;
+                    }
+                    first = __float_as_uint(r1.z), count = __float_as_uint(r1.w);
+                    continue;
+                }
+                if (okl && tl < h.best) {
+                    first = __float_as_uint(l1.z), count = __float_as_uint(l1.w);
+                    continue;
+                }
+            }
+            // pop until an entry passes tmin < closest
+            bool found = false;
+            while (sp > 0) {
+                sp--;
+                const uint32_t idx = stk[(sp * 2) * WAVE];
+                const float t = __uint_as_float(stk[(sp * 2 + 1) * WAVE]);
+                if (t < h.best) {
+                    const float4 nh = nodes4[2 * idx + 1];
+                    first = __float_as_uint(nh.z), count = __float_as_uint(nh.w);
+                    found = true;
+                    break;
+                }
+            }
+            if (!found) break;
+        }
+    }
+};
+
+// The per-pixel path tracer: raytracing_kernel_main + ray_color (main_raytracing.cu:111-200).
+template <class Tracer, int STACK, bool STATS>
+__device__ __forceinline__ void shade_pixel(const RenderArgs& a, uint32_t* stk, int x, int y, size_t rng_index,
+                                            size_t out_slot, Counters& c) {
     rt_rng_state* rs = a.rng + rng_index;
     rtm::Xorwow rng{rs->d, rs->v[0], rs->v[1], rs->v[2], rs->v[3], rs->v[4]};
-
     const rtm::f3 cam_o = ld3(a.cam.origin), cam_h = ld3(a.cam.horizontal), cam_v = ld3(a.cam.vertical),
                   cam_ll = ld3(a.cam.lower_left_corner);
     float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f, acc_a = 0.0f;
@@ -169,74 +336,35 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(RenderArgs a) {
         rtm::f3 ro = cam_o;
         rtm::f3 rd = rtm::sub(rtm::add(rtm::add(cam_ll, rtm::muls(cam_h, uvx)), rtm::muls(cam_v, uvy)), cam_o);
 
-        // ray_color (main_raytracing.cu:111-160)
         rtm::f3 color = rtm::mk(0, 0, 0), thr = rtm::mk(1, 1, 1);
         for (int bounce = 0; bounce < a.bounces; bounce++) {
-            n_seg++;
+            c.seg++;
             // GetRayHit (main_raytracing.cu:83-109)
             const rtm::f3 nd = rtm::normalize(rd);
-            float best = 1e30f;
-            int hit_kind = 0;  // 0 none, 1 sphere, 2 triangle
-            uint32_t hit_id = 0;
-            float hbx = 0.0f, hby = 0.0f;
-            for (int i = 0; i < a.sphere_count; i++) {
-                const GeometrySphere& sp = a.spheres[i];
-                float dist;
-                if (rtd::intersect_sphere(ro, nd, ld3(sp.position), sp.radius * sp.radius, &dist)) {
-                    if (dist >= best) continue;
-                    best = dist;
-                    hit_kind = 1;
-                    hit_id = (uint32_t)i;
-                    if (STATS) n_sacc++;
-                }
-            }
-            // BVHRayHit (main_raytracing.cu:33-81): DFS, right child popped first
-            int sp_top = 0;
-            stk[0] = 0u;
-            sp_top = 1;
-            while (sp_top) {
-                const GPUBVHNode& node = a.nodes[stk[(--sp_top) * BLOCK]];
-                if (STATS) n_node++;
-                if (!rtd::intersect_aabb(ro, rd, node.bmin, node.bmax, best)) continue;
-                if (node.prim_count > 0) {
-                    for (uint32_t i = 0; i < node.prim_count; i++) {
-                        const uint32_t fi = a.face_indices[node.first_index + i];
-                        const GPUFace f = a.faces[fi];
-                        float bx, by, dist;
-                        if (STATS) n_tri++;
-                        if (rtd::intersect_triangle(ro, nd, ld3(a.vertices[f.v0].position), ld3(a.vertices[f.v1].position),
-                                                    ld3(a.vertices[f.v2].position), &bx, &by, &dist)) {
-                            if (dist >= best || dist < 0.0f) continue;
-                            best = dist;
-                            hit_kind = 2;
-                            hit_id = fi;
-                            hbx = bx;
-                            hby = by;
-                            if (STATS) n_tacc++;
-                        }
-                    }
-                } else {
-                    stk[(sp_top++) * BLOCK] = node.first_index;
-                    stk[(sp_top++) * BLOCK] = node.first_index + 1;
-                }
-            }
+            Hit h;
+            h.best = 1e30f;
+            h.kind = 0;
+            h.id = 0;
+            h.bx = h.by = 0.0f;
+            trace_spheres<STATS>(a, ro, nd, h, c);
+            Tracer::template trace<STACK, STATS>(a, stk, ro, rd, nd, h, c);
 
-            if (hit_kind != 0) {
-                if (STATS) n_hit++;
-                // Hit attributes of the final closest hit (the reference recomputes them on
-                // every accept; only the last accept survives).
-                const rtm::f3 pos = rtm::add(ro, rtm::muls(nd, best));
+            if (h.kind != 0) {
+                if (STATS) c.hit++;
+                // Attributes of the final closest hit (the reference recomputes them on every
+                // accept; only the last accept survives, so computing them once is identical).
+                const rtm::f3 pos = rtm::add(ro, rtm::muls(nd, h.best));
                 rtm::f3 nrm;
                 uint32_t mat;
-                if (hit_kind == 1) {
-                    const GeometrySphere& sp = a.spheres[hit_id];
+                if (h.kind == 1) {
+                    const GeometrySphere& sp = a.spheres[h.id];
                     nrm = rtm::divs(rtm::sub(pos, ld3(sp.position)), sp.radius);
                     mat = (uint32_t)sp.material;
                 } else {
-                    const GPUFace f = a.faces[hit_id];
-                    const float bz = (1.0f - hbx) - hby;
-                    nrm = rtm::normalize(rtm::add(rtm::add(rtm::muls(ld3(a.vertices[f.v0].normal), hbx),
-                                                           rtm::muls(ld3(a.vertices[f.v1].normal), hby)),
+                    const GPUFace f = a.faces[h.id];
+                    const float bz = (1.0f - h.bx) - h.by;
+                    nrm = rtm::normalize(rtm::add(rtm::add(rtm::muls(ld3(a.vertices[f.v0].normal), h.bx),
+                                                           rtm::muls(ld3(a.vertices[f.v1].normal), h.by)),
                                                   rtm::muls(ld3(a.vertices[f.v2].normal), bz)));
                     if (rtm::dot(nd, nrm) >= 0.0f) nrm = rtm::neg(nrm);
                     mat = f.material;
@@ -264,12 +392,12 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(RenderArgs a) {
                 if (rng.uniform() > p) break;
                 thr = rtm::muls(thr, 1.0f / p);
             } else {
-                if (STATS) n_miss++;
+                if (STATS) c.miss++;
                 if (a.sky) {
                     const rtm::f3 dir = rtd::quat_rotate(a.qw, a.qx, a.qy, a.qz, rd);
-                    const rtm::f3 c = rtd::cube_sample(a.sky, a.sky_n, dir);
-                    const rtm::f3 cl = rtm::mk(rtm::gmin(rtm::gmax(c.x, 0.0f), 50.0f), rtm::gmin(rtm::gmax(c.y, 0.0f), 50.0f),
-                                               rtm::gmin(rtm::gmax(c.z, 0.0f), 50.0f));
+                    const rtm::f3 cs = rtd::cube_sample(a.sky, a.sky_n, dir);
+                    const rtm::f3 cl = rtm::mk(rtm::gmin(rtm::gmax(cs.x, 0.0f), 50.0f), rtm::gmin(rtm::gmax(cs.y, 0.0f), 50.0f),
+                                               rtm::gmin(rtm::gmax(cs.z, 0.0f), 50.0f));
                     color = rtm::add(color, rtm::mul(thr, cl));
                 }
                 break;
@@ -288,9 +416,8 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(RenderArgs a) {
     float4 prev;
     float4* out;
     if (a.out_shard) {
-        const size_t slot = (size_t)blockIdx.x * BLOCK + threadIdx.x;
-        prev = a.last ? reinterpret_cast<const float4*>(a.last)[slot] : make_float4(0, 0, 0, 0);
-        out = a.out_shard + slot;
+        prev = a.last ? reinterpret_cast<const float4*>(a.last)[out_slot] : make_float4(0, 0, 0, 0);
+        out = a.out_shard + out_slot;
     } else {
         prev = a.last ? *reinterpret_cast<const float4*>(a.last + (size_t)y * a.pitch + (size_t)x * 16)
                       : make_float4(0, 0, 0, 0);
@@ -305,23 +432,43 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(RenderArgs a) {
     rs->v[2] = rng.v2;
     rs->v[3] = rng.v3;
     rs->v[4] = rng.v4;
+}
 
-    }  // active pixel
-
+// One wave per workgroup; wave g renders the 8x8 sub-tile (g & 3) of shard tile (g >> 2).
+// The hardware dispatcher hands out the next sub-tile as soon as a wave retires, which
+// balances cheap (sky) against expensive (floor leaf) tiles.
+template <class Tracer, int STACK, bool STATS>
+__global__ __launch_bounds__(WAVE) void render_kernel(RenderArgs a) {
+    __shared__ uint32_t stack_lds[STACK * Tracer::WORDS * WAVE];
+    uint32_t* const stk = stack_lds + threadIdx.x;
+    const int g = (int)blockIdx.x;
+    const int k = g >> 2;
+    const int tid = ((g & 3) << 6) | (int)threadIdx.x;  // thread index within the 16x16 tile
+    const int tile = a.shard_index + k * a.shard_count;
+    int lx, ly;
+    tile_pixel(tid, &lx, &ly);
+    const int x = (tile % a.tiles_x) * TILE + lx;
+    const int y = (tile / a.tiles_x) * TILE + ly;
+    Counters c;
+    if (x < a.width && y < a.height) {  // off-frame lanes stay for the wave reduction
+        const size_t slot = (size_t)k * (TILE * TILE) + tid;
+        const size_t rng_index = a.shard_count == 1 ? (size_t)y * a.width + x : slot;
+        shade_pixel<Tracer, STACK, STATS>(a, stk, x, y, rng_index, slot, c);
+    }
     // Segment count (always on: the Mrays/s numerator), one atomic per wave.
     if (a.seg_counter) {
-        unsigned long long v = n_seg;
+        unsigned long long v = c.seg;
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if ((threadIdx.x & 63) == 0) atomicAdd(a.seg_counter, v);
+        if (threadIdx.x == 0) atomicAdd(a.seg_counter, v);
     }
     if (STATS) {
-        atomicAdd(a.stats + RT_STAT_SEGMENTS, n_seg);
-        atomicAdd(a.stats + RT_STAT_NODES, n_node);
-        atomicAdd(a.stats + RT_STAT_TRI_TESTS, n_tri);
-        atomicAdd(a.stats + RT_STAT_TRI_ACCEPTS, n_tacc);
-        atomicAdd(a.stats + RT_STAT_SPHERE_ACCEPTS, n_sacc);
-        atomicAdd(a.stats + RT_STAT_HITS, n_hit);
-        atomicAdd(a.stats + RT_STAT_MISSES, n_miss);
+        atomicAdd(a.stats + RT_STAT_SEGMENTS, c.seg);
+        atomicAdd(a.stats + RT_STAT_NODES, c.node);
+        atomicAdd(a.stats + RT_STAT_TRI_TESTS, c.tri);
+        atomicAdd(a.stats + RT_STAT_TRI_ACCEPTS, c.tacc);
+        atomicAdd(a.stats + RT_STAT_SPHERE_ACCEPTS, c.sacc);
+        atomicAdd(a.stats + RT_STAT_HITS, c.hit);
+        atomicAdd(a.stats + RT_STAT_MISSES, c.miss);
     }
 }
 
@@ -404,10 +551,22 @@ const uint32_t* device_jump_table() {
     return d;
 }
 
-template <int STACK, bool STATS>
-hipError_t launch(const RenderArgs& args, int blocks, hipStream_t stream) {
-    hipLaunchKernelGGL((render_kernel<STACK, STATS>), dim3(blocks), dim3(BLOCK), 0, stream, args);
+template <class Tracer, int STACK, bool STATS>
+hipError_t launch(const RenderArgs& args, int waves, hipStream_t stream) {
+    hipLaunchKernelGGL((render_kernel<Tracer, STACK, STATS>), dim3(waves), dim3(WAVE), 0, stream, args);
     return hipGetLastError();
+}
+
+template <class Tracer>
+hipError_t launch_variant(const RenderArgs& args, int waves, int depth, bool stats, hipStream_t s) {
+    // The DFS holds at most depth + 1 entries (one pending sibling per level).  Depth is known
+    // when the scene came through rt_scene_upload; otherwise use the reference's 64
+    // (main_raytracing.cu:35).
+    if (depth >= 0 && depth + 2 <= 28)
+        return stats ? launch<Tracer, 28, true>(args, waves, s) : launch<Tracer, 28, false>(args, waves, s);
+    if (depth >= 0 && depth + 2 <= 40)
+        return stats ? launch<Tracer, 40, true>(args, waves, s) : launch<Tracer, 40, false>(args, waves, s);
+    return stats ? launch<Tracer, 64, true>(args, waves, s) : launch<Tracer, 64, false>(args, waves, s);
 }
 
 int tiles_of_shard(int width, int height, int shard_index, int shard_count) {
@@ -477,19 +636,17 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     a.stats = (unsigned long long*)p->stats;
     a.seg_counter = (unsigned long long*)p->segment_counter;
 
-    const int blocks = tiles_of_shard(p->width, p->height, p->shard_index, p->shard_count);
-    if (blocks == 0) return 0;
-    // Stack: the DFS holds at most depth+1 entries.  Depth is known when the scene was
-    // uploaded through rt_scene_upload; otherwise use the reference's 64 (main_raytracing.cu:35).
-    const int depth = rt_internal_lookup_depth(scene->gpu_bvh_nodes);
-    const bool small = depth >= 0 && depth + 2 <= 32;
+    const int tiles = tiles_of_shard(p->width, p->height, p->shard_index, p->shard_count);
+    if (tiles == 0) return 0;
+    const void* tris = nullptr;
+    int depth = -1;
+    rt_internal_lookup_mirror(scene, &tris, &depth);
+    static const bool force_ref = std::getenv("RT_FORCE_REFERENCE_LAYOUT") != nullptr;  // A/B switch
+    a.tris = force_ref ? nullptr : (const FlatTri*)tris;
     const bool stats = (p->flags & RT_RENDER_STATS) != 0;
     hipStream_t s = (hipStream_t)stream;
-    hipError_t e;
-    if (small)
-        e = stats ? launch<32, true>(a, blocks, s) : launch<32, false>(a, blocks, s);
-    else
-        e = stats ? launch<64, true>(a, blocks, s) : launch<64, false>(a, blocks, s);
+    const hipError_t e = a.tris ? launch_variant<FlatTracer>(a, tiles * 4, depth, stats, s)
+                                : launch_variant<RefTracer>(a, tiles * 4, depth, stats, s);
     return check(e, "render_kernel launch");
 }
 

@@ -12,18 +12,39 @@
 #include <mutex>
 
 namespace {
-std::mutex g_depth_mutex;
-std::map<const void*, int> g_depth;
+struct Mirror {
+    const void* face_indices;
+    const void* vertices;
+    const void* faces;
+    const void* tris;
+    int depth;
+};
+std::mutex g_mirror_mutex;
+std::map<const void*, Mirror> g_mirrors;  // keyed by the device BVH node array
 }  // namespace
 
-void rt_internal_register_depth(const void* gpu_nodes, int depth) {
-    std::lock_guard<std::mutex> lock(g_depth_mutex);
-    g_depth[gpu_nodes] = depth;
+void rt_internal_register_mirror(const GPUScene* s, const void* tris, int depth) {
+    std::lock_guard<std::mutex> lock(g_mirror_mutex);
+    g_mirrors[s->gpu_bvh_nodes] = Mirror{s->gpu_bvh_face_indices, s->gpu_vertices, s->gpu_faces, tris, depth};
 }
-int rt_internal_lookup_depth(const void* gpu_nodes) {
-    std::lock_guard<std::mutex> lock(g_depth_mutex);
-    auto it = g_depth.find(gpu_nodes);
-    return it == g_depth.end() ? -1 : it->second;
+void rt_internal_forget_mirror(const void* gpu_nodes) {
+    std::lock_guard<std::mutex> lock(g_mirror_mutex);
+    g_mirrors.erase(gpu_nodes);
+}
+// The leaf-ordered triangle mirror is used only while ALL the reference arrays it was built
+// from are still the ones the GPUScene points at.
+bool rt_internal_lookup_mirror(const GPUScene* s, const void** tris, int* depth) {
+    std::lock_guard<std::mutex> lock(g_mirror_mutex);
+    auto it = g_mirrors.find(s->gpu_bvh_nodes);
+    *tris = nullptr;
+    *depth = -1;
+    if (it == g_mirrors.end()) return false;
+    const Mirror& m = it->second;
+    *depth = m.depth;
+    if (m.face_indices != s->gpu_bvh_face_indices || m.vertices != s->gpu_vertices || m.faces != s->gpu_faces)
+        return false;
+    *tris = m.tris;
+    return true;
 }
 
 namespace RayTracing {
@@ -213,6 +234,7 @@ Scene::Scene() {
     bvh = std::make_unique<BVH>();
 }
 Scene::~Scene() {
+    if (gpu_bvh_nodes) rt_internal_forget_mirror(gpu_bvh_nodes);
     if (environment) rt_cubemap_destroy(environment);
 }
 
@@ -319,8 +341,10 @@ void Scene::Upload(void* rng) {
     }
     environment_cubemap_tex = environment;
 
+    if (bvh_upload_pending || IsFlagDirty(DirtyFlagValue::SceneMemory)) tris_pending = true;
     if (bvh_upload_pending) {
         bvh_upload_pending = false;
+        if (gpu_bvh_nodes) rt_internal_forget_mirror(gpu_bvh_nodes);
         const size_t nb = bvh->GetNodeCount() * sizeof(GPUBVHNode);
         bvh_memory = std::make_unique<DeviceMemory>(nb);
         gpu_bvh_nodes = (const GPUBVHNode*)bvh_memory->GetMemory();
@@ -329,7 +353,6 @@ void Scene::Upload(void* rng) {
         bvh_face_index_memory = std::make_unique<DeviceMemory>(ni);
         gpu_bvh_face_indices = (const uint32_t*)bvh_face_index_memory->GetMemory();
         upload(*bvh_face_index_memory, bvh->GetFaceIndices().data(), ni);
-        rt_internal_register_depth(gpu_bvh_nodes, bvh->GetMaxDepth());
     }
     if (IsFlagDirty(DirtyFlagValue::SceneMemory)) {
         const size_t ns = spheres.size() * sizeof(GeometrySphere);
@@ -351,6 +374,29 @@ void Scene::Upload(void* rng) {
         faces_memory = std::make_unique<DeviceMemory>(nf);
         gpu_faces = (const GPUFace*)faces_memory->GetMemory();
         upload(*faces_memory, faces.data(), nf);
+    }
+    if (tris_pending) {
+        // Leaf-ordered triangle mirror (kernel FlatTri): for BVH slot i, face f =
+        // face_indices[i]: (v0.xyz, e1.x), (e1.yz, e2.xy), (e2.z, f, 0, 0) with e1 = v1 - v0,
+        // e2 = v2 - v0 as glm::intersectRayTriangle forms them (gtx/intersect.inl:37-38).
+        const std::vector<uint32_t>& fi = bvh->GetFaceIndices();
+        std::vector<float> t(fi.size() * 12, 0.0f);
+        for (size_t i = 0; i < fi.size(); i++) {
+            const GPUFace& f = faces[fi[i]];
+            const float* p0 = vertices[f.v0].position;
+            const float* p1 = vertices[f.v1].position;
+            const float* p2 = vertices[f.v2].position;
+            float* o = &t[i * 12];
+            o[0] = p0[0], o[1] = p0[1], o[2] = p0[2];
+            o[3] = p1[0] - p0[0], o[4] = p1[1] - p0[1], o[5] = p1[2] - p0[2];
+            o[6] = p2[0] - p0[0], o[7] = p2[1] - p0[1], o[8] = p2[2] - p0[2];
+            uint32_t id = fi[i];
+            std::memcpy(&o[9], &id, 4);
+        }
+        tris_memory = std::make_unique<DeviceMemory>(t.size() * sizeof(float));
+        upload(*tris_memory, t.data(), t.size() * sizeof(float));
+        rt_internal_register_mirror(this, tris_memory->GetMemory(), bvh->GetMaxDepth());
+        tris_pending = false;
     }
     dirty_flags = 0;
 }

@@ -131,7 +131,7 @@ struct Scene : public GPUScene {
     std::vector<GPUFace> faces;
     std::vector<GPUVertex> vertices;
     std::unique_ptr<DeviceMemory> memory, materials_memory, bvh_memory, bvh_face_index_memory, faces_memory,
-        vertices_memory;
+        vertices_memory, tris_memory;
     uint64_t environment = 0;
     std::vector<float> environment_texels;
     int environment_size = 0;
@@ -139,6 +139,7 @@ struct Scene : public GPUScene {
     std::unique_ptr<BVH> bvh;
     DirtyFlags dirty_flags = ~0u;
     bool bvh_upload_pending = false;
+    bool tris_pending = false;
 };
 
 // CUDARayTracer::SetupCornellBox / SetupStanfordBunny (RayTracing/RayTracing.cpp:79-203, 33-69)
@@ -150,6 +151,8 @@ void SetupPlaneGrid(Scene& scene, int n);
 
 }  // namespace RayTracing
 
-// Max BVH depth registered by Scene::Upload for a device node array (kernel stack sizing).
-int rt_internal_lookup_depth(const void* gpu_nodes);
-void rt_internal_register_depth(const void* gpu_nodes, int depth);
+// Leaf-ordered triangle mirror + BVH depth registered by Scene::Upload for the device
+// arrays of a GPUScene (kernel fast path and stack sizing; see rt_kernel.hip).
+void rt_internal_register_mirror(const GPUScene* scene, const void* tris, int depth);
+void rt_internal_forget_mirror(const void* gpu_nodes);
+bool rt_internal_lookup_mirror(const GPUScene* scene, const void** tris, int* depth);
