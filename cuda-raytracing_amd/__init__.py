@@ -25,6 +25,7 @@ LIB_PATH = os.path.join(PKG_DIR, "librt_hip.so")
 ASSETS_DIR = os.path.join(ROOT_DIR, "assets")
 
 RT_RENDER_STATS = 1
+TRACERS = {"fast": 0, "ref": 2, "flat": 4}  # rt_render_params.flags
 STAT_NAMES = ("segments", "nodes", "tri_tests", "tri_accepts", "sphere_accepts", "hits", "misses")
 SCENES = {"bunny": 0, "bunny4": 1, "plane1m": 2}
 
@@ -258,7 +259,7 @@ def init_rng_states(rng, width, height, seed, shard_index=0, shard_count=1, stre
 
 
 def render(scene, surface, last, width, height, spp, bounces, frame_index=0, shard_index=0, shard_count=1,
-           out_shard=None, stats=None, segment_counter=None, stream=None):
+           out_shard=None, stats=None, segment_counter=None, stream=None, tracer="fast"):
     """rt_render: one frame (or one shard of it) on `stream` (default: torch's current stream)."""
     p = RenderParams()
     p.surface = surface.data_ptr() if surface is not None else None
@@ -268,10 +269,11 @@ def render(scene, surface, last, width, height, spp, bounces, frame_index=0, sha
     p.frame_index, p.spp, p.bounces = frame_index, spp, bounces
     p.shard_index, p.shard_count = shard_index, shard_count
     p.out_shard = out_shard.data_ptr() if out_shard is not None else None
+    p.flags = TRACERS[tracer]
     if segment_counter is not None:
         p.segment_counter = segment_counter.data_ptr()
     if stats is not None:
-        p.flags = RT_RENDER_STATS
+        p.flags |= RT_RENDER_STATS
         p.stats = stats.data_ptr()
     _check(lib().rt_render(ctypes.byref(p), ctypes.cast(scene.gpu, ctypes.c_void_p), _stream_ptr(stream)), "rt_render")
 

@@ -25,8 +25,9 @@
 #include "rt_device.h"
 #include "rt_math.h"
 #include "xorwow.h"
+#include "rt_fast.h"
 
-bool rt_internal_lookup_mirror(const GPUScene* scene, const void** tris, int* depth);
+bool rt_internal_lookup_mirror(const GPUScene* scene, const void** tris, int* depth, bool* scene_fast);
 
 // ---------------------------------------------------------------------------------------
 // error state
@@ -137,6 +138,7 @@ struct RenderArgs {
     int shard_index, shard_count, tiles_x;
     unsigned long long* stats;
     unsigned long long* seg_counter;
+    int scene_fast;  // all node bounds inside the filtered-slab range (rt_fast.h)
 };
 
 struct Counters {
@@ -472,6 +474,193 @@ __global__ __launch_bounds__(WAVE) void render_kernel(RenderArgs a) {
     }
 }
 
+// The production kernel: rt_fast.h traversal + a flat per-lane segment loop.
+// raytracing_kernel_main / ray_color (main_raytracing.cu:111-200) nest `for sample { for
+// bounce { ... break } }`; on a SIMD machine that makes every lane wait at the end of each
+// sample for the longest path of the wave.  Here each lane runs a small state machine --
+// start a camera sample, trace a segment, shade, end the path on a miss / Russian roulette /
+// the bounce limit, start its next sample -- so a lane only idles once its whole pixel is
+// done.  The per-pixel draw order (u, v, then 4 draws per hit) is the reference's.
+template <int STACK, bool STATS>
+__global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
+    __shared__ uint32_t stack_lds[STACK * 2 * WAVE];
+    uint32_t* const stk = stack_lds + threadIdx.x;
+    const float4* nodes4 = reinterpret_cast<const float4*>(a.nodes);
+    const float4* tris = reinterpret_cast<const float4*>(a.tris);
+    const int g = (int)blockIdx.x;
+    const int k = g >> 2;
+    const int tid = ((g & 3) << 6) | (int)threadIdx.x;
+    const int tile = a.shard_index + k * a.shard_count;
+    int lx, ly;
+    tile_pixel(tid, &lx, &ly);
+    const int x = (tile % a.tiles_x) * TILE + lx;
+    const int y = (tile / a.tiles_x) * TILE + ly;
+    Counters c;
+    bool pixel = x < a.width && y < a.height;
+    const size_t slot = (size_t)k * (TILE * TILE) + tid;
+    rt_rng_state* rs = a.rng + (a.shard_count == 1 ? (size_t)(pixel ? y : 0) * a.width + (pixel ? x : 0) : slot);
+    rtm::Xorwow rng{0, 0, 0, 0, 0, 0};
+    if (pixel) rng = rtm::Xorwow{rs->d, rs->v[0], rs->v[1], rs->v[2], rs->v[3], rs->v[4]};
+    const rtm::f3 cam_o = ld3(a.cam.origin), cam_h = ld3(a.cam.horizontal), cam_v = ld3(a.cam.vertical),
+                  cam_ll = ld3(a.cam.lower_left_corner);
+    float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f, acc_a = 0.0f;
+    int sample = 0, bounce = 0;
+    bool path = false;
+    rtm::f3 ro = cam_o, rd = cam_o, color = rtm::mk(0, 0, 0), thr = rtm::mk(1, 1, 1);
+    const bool scene_fast = a.scene_fast != 0;
+
+    for (;;) {
+        if (pixel && !path) {
+            if (sample < a.spp) {
+                // main_raytracing.cu:190: uv = (pixel + vec2(rng(), rng())) / vec2(W, H), u first
+                const float ru = rng.uniform();
+                const float rv = rng.uniform();
+                const float uvx = ((float)x + ru) / (float)a.width;
+                const float uvy = ((float)y + rv) / (float)a.height;
+                ro = cam_o;  // GPUCamera::GetRay (GPUScene.h:13), not normalized
+                rd = rtm::sub(rtm::add(rtm::add(cam_ll, rtm::muls(cam_h, uvx)), rtm::muls(cam_v, uvy)), cam_o);
+                color = rtm::mk(0, 0, 0);
+                thr = rtm::mk(1, 1, 1);
+                bounce = 0;
+                path = true;
+                if (a.bounces == 0) {  // an empty bounce loop: the sample contributes (0,0,0,1)
+                    acc_a += 1.0f;
+                    sample++;
+                    path = false;
+                    continue;
+                }
+            } else {
+                pixel = false;
+                // main_raytracing.cu:195-199
+                const float fs = (float)a.spp;
+                const rtm::f4 res{acc_r / fs, acc_g / fs, acc_b / fs, acc_a / fs};
+                const float lerp = a.frame_index > 0 ? 1.0f / (float)(a.frame_index + 1) : 1.0f;
+                float4 prev;
+                float4* out;
+                if (a.out_shard) {
+                    prev = a.last ? reinterpret_cast<const float4*>(a.last)[slot] : make_float4(0, 0, 0, 0);
+                    out = a.out_shard + slot;
+                } else {
+                    prev = a.last ? *reinterpret_cast<const float4*>(a.last + (size_t)y * a.pitch + (size_t)x * 16)
+                                  : make_float4(0, 0, 0, 0);
+                    out = reinterpret_cast<float4*>(a.surface + (size_t)y * a.pitch + (size_t)x * 16);
+                }
+                const rtm::f4 o = rtm::mix4(rtm::f4{prev.x, prev.y, prev.z, prev.w}, res, lerp);
+                *out = make_float4(o.x, o.y, o.z, 1.0f);
+                rs->d = rng.d;
+                rs->v[0] = rng.v0;
+                rs->v[1] = rng.v1;
+                rs->v[2] = rng.v2;
+                rs->v[3] = rng.v3;
+                rs->v[4] = rng.v4;
+            }
+        }
+        if (!__ballot(path)) break;
+
+        // GetRayHit (main_raytracing.cu:83-109)
+        rtfast::Hit h;
+        h.best = 1e30f, h.kind = 0, h.id = 0, h.bx = h.by = 0.0f;
+        const rtm::f3 nd = rtm::normalize(rd);
+        if (path) {
+            c.seg++;
+            for (int i = 0; i < a.sphere_count; i++) {
+                const GeometrySphere& sp = a.spheres[i];
+                float dist;
+                if (rtd::intersect_sphere(ro, nd, ld3(sp.position), sp.radius * sp.radius, &dist)) {
+                    if (dist >= h.best) continue;
+                    h.best = dist;
+                    h.kind = 1;
+                    h.id = (uint32_t)i;
+                    if (STATS) c.sacc++;
+                }
+            }
+        }
+        const rtfast::Ray R = rtfast::make_ray(ro, rd, nd, scene_fast);
+        rtfast::trace<WAVE, STATS>(nodes4, tris, stk, R, h, path, c);
+        if (!path) continue;
+
+        bool end = false;
+        if (h.kind != 0) {
+            if (STATS) c.hit++;
+            const rtm::f3 pos = rtm::add(ro, rtm::muls(nd, h.best));
+            rtm::f3 nrm;
+            uint32_t mat;
+            if (h.kind == 1) {
+                const GeometrySphere& sp = a.spheres[h.id];
+                nrm = rtm::divs(rtm::sub(pos, ld3(sp.position)), sp.radius);
+                mat = (uint32_t)sp.material;
+            } else {
+                const GPUFace f = a.faces[h.id];
+                const float bz = (1.0f - h.bx) - h.by;
+                nrm = rtm::normalize(rtm::add(rtm::add(rtm::muls(ld3(a.vertices[f.v0].normal), h.bx),
+                                                       rtm::muls(ld3(a.vertices[f.v1].normal), h.by)),
+                                              rtm::muls(ld3(a.vertices[f.v2].normal), bz)));
+                if (rtm::dot(nd, nrm) >= 0.0f) nrm = rtm::neg(nrm);
+                mat = f.material;
+            }
+            const GPUMaterial& m = a.materials[mat];
+            const float do_spec = (rng.uniform() < m.specular_percent) ? 1.0f : 0.0f;
+            color = rtm::add(color, rtm::mul(thr, ld3(m.emissive)));
+            const float om = 1.0f - do_spec;
+            thr = rtm::mul(thr, rtm::mk(m.albedo[0] * om + m.specular[0] * do_spec,
+                                        m.albedo[1] * om + m.specular[1] * do_spec,
+                                        m.albedo[2] * om + m.specular[2] * do_spec));
+            // GetRandomPointOnSphere (Random.h:23-46)
+            const float zz = rng.uniform() * 2.0f - 1.0f;
+            const float ang = rng.uniform() * 3.141592654f * 2.0f;
+            const float rr = sqrtf(1.0f - zz * zz);
+            const rtm::f3 sph = rtm::mk(rr * rtm::rt_cosf(ang), rr * rtm::rt_sinf(ang), zz);
+            const rtm::f3 diffuse = rtm::normalize(rtm::add(nrm, sph));
+            rtm::f3 spec = rtm::normalize(rtm::reflect(rd, nrm));
+            spec = rtm::normalize(rtm::mix(spec, diffuse, m.roughness * m.roughness));
+            const rtm::f3 ndir = rtm::normalize(rtm::add(rtm::muls(diffuse, om), rtm::muls(spec, do_spec)));
+            ro = rtm::add(pos, rtm::muls(nrm, 0.01f));
+            rd = ndir;
+            // Russian roulette (main_raytracing.cu:140-148)
+            const float p = rtm::gmax(thr.x, rtm::gmax(thr.y, thr.z));
+            if (rng.uniform() > p) {
+                end = true;
+            } else {
+                thr = rtm::muls(thr, 1.0f / p);
+            }
+        } else {
+            if (STATS) c.miss++;
+            if (a.sky) {
+                const rtm::f3 dir = rtd::quat_rotate(a.qw, a.qx, a.qy, a.qz, rd);
+                const rtm::f3 cs = rtd::cube_sample(a.sky, a.sky_n, dir);
+                const rtm::f3 cl = rtm::mk(rtm::gmin(rtm::gmax(cs.x, 0.0f), 50.0f), rtm::gmin(rtm::gmax(cs.y, 0.0f), 50.0f),
+                                           rtm::gmin(rtm::gmax(cs.z, 0.0f), 50.0f));
+                color = rtm::add(color, rtm::mul(thr, cl));
+            }
+            end = true;
+        }
+        if (++bounce >= a.bounces) end = true;
+        if (end) {
+            acc_r += color.x;
+            acc_g += color.y;
+            acc_b += color.z;
+            acc_a += 1.0f;
+            sample++;
+            path = false;
+        }
+    }
+
+    if (a.seg_counter) {
+        unsigned long long v = c.seg;
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (threadIdx.x == 0) atomicAdd(a.seg_counter, v);
+    }
+    if (STATS) {
+        atomicAdd(a.stats + RT_STAT_SEGMENTS, c.seg);
+        atomicAdd(a.stats + RT_STAT_NODES, c.node);
+        atomicAdd(a.stats + RT_STAT_TRI_TESTS, c.tri);
+        atomicAdd(a.stats + RT_STAT_TRI_ACCEPTS, c.tacc);
+        atomicAdd(a.stats + RT_STAT_SPHERE_ACCEPTS, c.sacc);
+        atomicAdd(a.stats + RT_STAT_HITS, c.hit);
+        atomicAdd(a.stats + RT_STAT_MISSES, c.miss);
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // init_rng (Random.cu:3-13): state s <- curand_init(seed, pixel(s), 0)
 // ---------------------------------------------------------------------------------------
@@ -557,6 +746,20 @@ hipError_t launch(const RenderArgs& args, int waves, hipStream_t stream) {
     return hipGetLastError();
 }
 
+template <int STACK, bool STATS>
+hipError_t launch_fast_t(const RenderArgs& args, int waves, hipStream_t stream) {
+    hipLaunchKernelGGL((render_fast_kernel<STACK, STATS>), dim3(waves), dim3(WAVE), 0, stream, args);
+    return hipGetLastError();
+}
+
+hipError_t launch_fast(const RenderArgs& args, int waves, int depth, bool stats, hipStream_t s) {
+    if (depth >= 0 && depth + 2 <= 28)
+        return stats ? launch_fast_t<28, true>(args, waves, s) : launch_fast_t<28, false>(args, waves, s);
+    if (depth >= 0 && depth + 2 <= 40)
+        return stats ? launch_fast_t<40, true>(args, waves, s) : launch_fast_t<40, false>(args, waves, s);
+    return stats ? launch_fast_t<64, true>(args, waves, s) : launch_fast_t<64, false>(args, waves, s);
+}
+
 template <class Tracer>
 hipError_t launch_variant(const RenderArgs& args, int waves, int depth, bool stats, hipStream_t s) {
     // The DFS holds at most depth + 1 entries (one pending sibling per level).  Depth is known
@@ -640,13 +843,23 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     if (tiles == 0) return 0;
     const void* tris = nullptr;
     int depth = -1;
-    rt_internal_lookup_mirror(scene, &tris, &depth);
+    bool scene_fast = false;
+    rt_internal_lookup_mirror(scene, &tris, &depth, &scene_fast);
     static const bool force_ref = std::getenv("RT_FORCE_REFERENCE_LAYOUT") != nullptr;  // A/B switch
     a.tris = force_ref ? nullptr : (const FlatTri*)tris;
     const bool stats = (p->flags & RT_RENDER_STATS) != 0;
     hipStream_t s = (hipStream_t)stream;
-    const hipError_t e = a.tris ? launch_variant<FlatTracer>(a, tiles * 4, depth, stats, s)
-                                : launch_variant<RefTracer>(a, tiles * 4, depth, stats, s);
+    static const char* which = std::getenv("RT_TRACER");  // A/B switch: ref | flat | fast (default)
+    const bool want_flat = (p->flags & RT_RENDER_TRACER_FLAT) || (which && std::strcmp(which, "flat") == 0);
+    if ((p->flags & RT_RENDER_TRACER_REF) || (which && std::strcmp(which, "ref") == 0)) a.tris = nullptr;
+    a.scene_fast = scene_fast ? 1 : 0;
+    hipError_t e;
+    if (!a.tris)
+        e = launch_variant<RefTracer>(a, tiles * 4, depth, stats, s);
+    else if (want_flat)
+        e = launch_variant<FlatTracer>(a, tiles * 4, depth, stats, s);
+    else
+        e = launch_fast(a, tiles * 4, depth, stats, s);
     return check(e, "render_kernel launch");
 }
 

@@ -4,6 +4,7 @@
 #include "scene.h"
 
 #include <algorithm>
+#include <cmath>
 #include <array>
 #include <cstdio>
 #include <cstring>
@@ -18,14 +19,15 @@ struct Mirror {
     const void* faces;
     const void* tris;
     int depth;
+    bool fast;
 };
 std::mutex g_mirror_mutex;
 std::map<const void*, Mirror> g_mirrors;  // keyed by the device BVH node array
 }  // namespace
 
-void rt_internal_register_mirror(const GPUScene* s, const void* tris, int depth) {
+void rt_internal_register_mirror(const GPUScene* s, const void* tris, int depth, bool fast) {
     std::lock_guard<std::mutex> lock(g_mirror_mutex);
-    g_mirrors[s->gpu_bvh_nodes] = Mirror{s->gpu_bvh_face_indices, s->gpu_vertices, s->gpu_faces, tris, depth};
+    g_mirrors[s->gpu_bvh_nodes] = Mirror{s->gpu_bvh_face_indices, s->gpu_vertices, s->gpu_faces, tris, depth, fast};
 }
 void rt_internal_forget_mirror(const void* gpu_nodes) {
     std::lock_guard<std::mutex> lock(g_mirror_mutex);
@@ -33,14 +35,16 @@ void rt_internal_forget_mirror(const void* gpu_nodes) {
 }
 // The leaf-ordered triangle mirror is used only while ALL the reference arrays it was built
 // from are still the ones the GPUScene points at.
-bool rt_internal_lookup_mirror(const GPUScene* s, const void** tris, int* depth) {
+bool rt_internal_lookup_mirror(const GPUScene* s, const void** tris, int* depth, bool* fast) {
     std::lock_guard<std::mutex> lock(g_mirror_mutex);
     auto it = g_mirrors.find(s->gpu_bvh_nodes);
     *tris = nullptr;
     *depth = -1;
+    *fast = false;
     if (it == g_mirrors.end()) return false;
     const Mirror& m = it->second;
     *depth = m.depth;
+    *fast = m.fast;
     if (m.face_indices != s->gpu_bvh_face_indices || m.vertices != s->gpu_vertices || m.faces != s->gpu_faces)
         return false;
     *tris = m.tris;
@@ -395,7 +399,17 @@ void Scene::Upload(void* rng) {
         }
         tris_memory = std::make_unique<DeviceMemory>(t.size() * sizeof(float));
         upload(*tris_memory, t.data(), t.size() * sizeof(float));
-        rt_internal_register_mirror(this, tris_memory->GetMemory(), bvh->GetMaxDepth());
+        // rt_fast.h filtered slab tests need every node bound component to be 0 or have a
+        // magnitude in [2^-60, 2^62]; otherwise the kernel uses exact quotients throughout.
+        bool fast = true;
+        const GPUBVHNode* bn = bvh->GetGPUBVHNodes();
+        for (size_t n = 0; n < bvh->GetNodeCount() && fast; n++)
+            for (int k = 0; k < 3; k++) {
+                const float lo = std::fabs(bn[n].bmin[k]), hi = std::fabs(bn[n].bmax[k]);
+                if ((lo != 0.0f && (lo < 0x1p-60f || lo > 0x1p62f)) || (hi != 0.0f && (hi < 0x1p-60f || hi > 0x1p62f)))
+                    fast = false;
+            }
+        rt_internal_register_mirror(this, tris_memory->GetMemory(), bvh->GetMaxDepth(), fast);
         tris_pending = false;
     }
     dirty_flags = 0;

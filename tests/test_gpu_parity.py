@@ -31,7 +31,7 @@ def make_scene(rt, which, w, h, plane_n=None):
     return s
 
 
-def gpu_render(rt, which, w, h, spp, bounces, frames=1, plane_n=None, seed=T.SEED, stats=False):
+def gpu_render(rt, which, w, h, spp, bounces, frames=1, plane_n=None, seed=T.SEED, stats=False, tracer="fast"):
     s = make_scene(rt, which, w, h, plane_n)
     rng = rt.alloc_rng(w * h)
     rt.init_rng_states(rng, w, h, seed)
@@ -41,7 +41,7 @@ def gpu_render(rt, which, w, h, spp, bounces, frames=1, plane_n=None, seed=T.SEE
     outs = []
     for f in range(frames):
         cur, prev = (a, b) if f % 2 == 0 else (b, a)
-        rt.render(s, cur, prev, w, h, spp, bounces, frame_index=f, stats=st)
+        rt.render(s, cur, prev, w, h, spp, bounces, frame_index=f, stats=st, tracer=tracer)
         outs.append(rt.surface_view(cur, w).cpu().numpy().copy())
     torch.cuda.synchronize()
     res = {"frames": outs, "rng": rng.view(-1, 12)[:, :6].cpu().numpy().view(np.uint32).copy()}
@@ -89,10 +89,13 @@ def test_init_rng_reference_entry_point(rt):
         assert np.array_equal(got[i], T.oracle_rng_state(12345, i)), i
 
 
+@pytest.mark.parametrize("tracer", ["fast", "flat", "ref"])
 @pytest.mark.parametrize("spp,bounces", [(1, 1), (4, 6), (8, 6)])
-def test_render_bunny_small(rt, spp, bounces):
+def test_render_bunny_small(rt, spp, bounces, tracer):
+    """Every kernel variant (production fast path, exact-division flat path, reference-layout
+    path) against the oracle, including the traversal counts."""
     w, h = 64, 36
-    g = gpu_render(rt, "bunny", w, h, spp, bounces, stats=True)
+    g = gpu_render(rt, "bunny", w, h, spp, bounces, stats=True, tracer=tracer)
     o = oracle_render("bunny", w, h, spp, bounces)
     assert_close(g["frames"][0], o["frames"][0], f"bunny {w}x{h} spp{spp} b{bounces}")
     assert np.array_equal(g["rng"], o["rng"]), "final RNG states differ"
@@ -165,6 +168,18 @@ def test_plane_grid_small(rt):
     g = gpu_render(rt, "plane1m", 40, 24, 1, 6, plane_n=64)
     o = oracle_render("plane1m", 40, 24, 1, 6, plane_n=64)
     assert_close(g["frames"][0], o["frames"][0], "plane grid 64")
+
+
+@pytest.mark.parametrize("which,plane_n", [("bunny", None), ("bunny4", None), ("plane1m", 200)])
+def test_tracers_agree_medium(rt, which, plane_n):
+    """256x144, 4 spp, 6 bounces: the three kernel variants produce identical frames and RNG
+    states (a larger sample of rays than the oracle comparisons above)."""
+    res = {t: gpu_render(rt, which, 256, 144, 4, 6, plane_n=plane_n, stats=True, tracer=t)
+           for t in ("fast", "flat", "ref")}
+    for t in ("flat", "ref"):
+        assert np.array_equal(res["fast"]["frames"][0], res[t]["frames"][0]), t
+        assert np.array_equal(res["fast"]["rng"], res[t]["rng"]), t
+        assert np.array_equal(res["fast"]["stats"][:7], res[t]["stats"][:7]), t
 
 
 def test_full_size_config2_properties(rt):
