@@ -145,7 +145,7 @@ def main():
 
     # --- exact traversal counts of one frame (stats kernel variant) on a copy of the RNG state
     rng_saved = rng.clone()
-    stats = torch.zeros(8, dtype=torch.int64, device=dev)
+    stats = torch.zeros(16, dtype=torch.int64, device=dev)
     if sharded:
         rt.render(scene, None, bufs[1], W, H, SPP, BOUNCES, 0, rank, world, out_shard=bufs[0], stats=stats)
     else:
@@ -233,7 +233,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config),
                          "kernel": "render_kernel", "kernel_ms": round(kern_avg_s * 1e3, 3),
                          "algorithmic_bytes_per_launch": int(bytes_per_launch),
-                         "frame0_counts": {k: int(v) for k, v in zip(rt.STAT_NAMES, stats0[:7])}},
+                         "frame0_counts": {k: int(v) for k, v in zip(rt.STAT_NAMES, stats0) if k}},
             "setup_s": round(setup_s, 2),
             "image_finite": finite,
         }

@@ -56,7 +56,7 @@ def build_product(force=False):
     for src in HIP_SOURCES:
         obj = os.path.join(BUILD, src + ".o")
         _run([HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *FP_FLAGS,
-              "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics", "-I", INC, "-I", CSRC,
+              "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics", "-fno-slp-vectorize", "-I", INC, "-I", CSRC,
               "-c", os.path.join(CSRC, src), "-o", obj])
         objs.append(obj)
     for src in HOST_SOURCES:

@@ -111,10 +111,17 @@ __device__ __forceinline__ void test_triangle(const Ray& R, float4 A, float4 B, 
     const f3 perp = rtm::cross(dist, e1);
     const float v = rtm::dot(R.nd, perp);
     const float uv = u + v;
-    const bool pos = det > eps && !(u < 0.0f || u > det) && !(v < 0.0f || uv > det);
-    const bool neg = det < -eps && !(u > 0.0f || u < det) && !(v > 0.0f || uv < det);
+    // det > eps: !(u < 0 || u > det) && !(v < 0 || u+v > det); det < -eps: the same with every
+    // inequality reversed.  Flipping the signs of u, v, u+v and det by det's sign bit maps the
+    // second case onto the first exactly (negation is exact; NaN compares stay false).
+    const uint32_t sgn = __float_as_uint(det) & 0x80000000u;
+    const float adet = fabsf(det);
+    const float su = __uint_as_float(__float_as_uint(u) ^ sgn);
+    const float sv = __uint_as_float(__float_as_uint(v) ^ sgn);
+    const float suv = __uint_as_float(__float_as_uint(uv) ^ sgn);
+    const bool ok = adet > eps && !(su < 0.0f || su > adet) && !(sv < 0.0f || suv > adet);
     if (STATS) c.tri++;
-    if (pos || neg) {
+    if (ok) {
         const float inv_det = 1.0f / det;
         const float t = rtm::dot(e2, perp) * inv_det;
         if (!(t >= h.best || t < 0.0f)) {
@@ -245,6 +252,10 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
     for (;;) {
         const bool small = active && count <= (uint32_t)BIG;
         if (__ballot(small)) {
+            if (STATS) {
+                c.w_small += threadIdx.x == 0;
+                c.l_small += small;
+            }
             if (small) {
                 if (count > 0) {
                     for (uint32_t i = first; i < first + count; i++)
@@ -259,13 +270,26 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
         const unsigned long long big = __ballot(active);
         if (!big) break;
         // every waiting lane is at a big leaf: run them together
-        const uint32_t f0 = __builtin_amdgcn_readfirstlane(first);
-        const uint32_t c0 = __builtin_amdgcn_readfirstlane(count);
+        // the leaf of the lowest waiting lane (not lane 0: it may be done, with stale state)
+        const int l0 = __ffsll((long long)big) - 1;
+        const uint32_t f0 = __builtin_amdgcn_readlane(first, l0);
+        const uint32_t c0 = __builtin_amdgcn_readlane(count, l0);
+        if (STATS) {
+            uint32_t mx = active ? count : 0u;
+            for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
+            c.w_big += threadIdx.x == 0 ? mx : 0;
+            c.l_big += active ? count : 0;
+        }
         if (__ballot(active && first == f0) == big) {
+            // all waiting lanes share one leaf: scalar loads, next record prefetched
             ConstF4 st = (ConstF4)(tris + 3 * (size_t)f0);
+            ConstF4 const last = st + 3 * (c0 - 1);
+            float4 A = ldc(st, 0), B = ldc(st, 1), Cc = ldc(st, 2);
             for (uint32_t i = 0; i < c0; i++) {
-                const float4 A = ldc(st, 3 * i), B = ldc(st, 3 * i + 1), Cc = ldc(st, 3 * i + 2);
+                st = st == last ? st : st + 3;
+                const float4 An = ldc(st, 0), Bn = ldc(st, 1), Cn = ldc(st, 2);
                 if (active) test_triangle<STATS>(R, A, B, Cc, h, c);
+                A = An, B = Bn, Cc = Cn;
             }
         } else if (active) {
             for (uint32_t i = first; i < first + count; i++)

@@ -143,6 +143,7 @@ struct RenderArgs {
 
 struct Counters {
     unsigned long long seg = 0, node = 0, tri = 0, tacc = 0, sacc = 0, hit = 0, miss = 0;
+    unsigned long long w_small = 0, l_small = 0, w_big = 0, l_big = 0, w_seg = 0, l_seg = 0;
 };
 
 struct Hit {
@@ -556,6 +557,10 @@ __global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
             }
         }
         if (!__ballot(path)) break;
+        if (STATS) {
+            c.w_seg += threadIdx.x == 0;
+            c.l_seg += path;
+        }
 
         // GetRayHit (main_raytracing.cu:83-109)
         rtfast::Hit h;
@@ -658,6 +663,12 @@ __global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
         atomicAdd(a.stats + RT_STAT_SPHERE_ACCEPTS, c.sacc);
         atomicAdd(a.stats + RT_STAT_HITS, c.hit);
         atomicAdd(a.stats + RT_STAT_MISSES, c.miss);
+        atomicAdd(a.stats + RT_STAT_WAVE_SMALL_ITERS, c.w_small);
+        atomicAdd(a.stats + RT_STAT_LANE_SMALL, c.l_small);
+        atomicAdd(a.stats + RT_STAT_WAVE_BIG_TRIS, c.w_big);
+        atomicAdd(a.stats + RT_STAT_LANE_BIG_TRIS, c.l_big);
+        atomicAdd(a.stats + RT_STAT_WAVE_SEGMENT_ITERS, c.w_seg);
+        atomicAdd(a.stats + RT_STAT_LANE_SEGMENTS, c.l_seg);
     }
 }
 

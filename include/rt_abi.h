@@ -180,7 +180,14 @@ enum {
     RT_STAT_SPHERE_ACCEPTS = 4,
     RT_STAT_HITS = 5,       /* segments that hit something */
     RT_STAT_MISSES = 6,     /* segments that sampled the sky */
-    RT_STAT_COUNT = 8
+    /* SIMD-efficiency counters of the fast kernel (wave-level iterations, active lanes) */
+    RT_STAT_WAVE_SMALL_ITERS = 8,   /* traversal steps (inner nodes / small leaves) */
+    RT_STAT_LANE_SMALL = 9,
+    RT_STAT_WAVE_BIG_TRIS = 10,     /* big-leaf triangle iterations */
+    RT_STAT_LANE_BIG_TRIS = 11,
+    RT_STAT_WAVE_SEGMENT_ITERS = 12,/* segment-loop iterations */
+    RT_STAT_LANE_SEGMENTS = 13,
+    RT_STAT_COUNT = 16
 };
 
 /* Render on `stream` (a hipStream_t, NULL = null stream).  Returns 0 or an error code. */
