@@ -1,0 +1,64 @@
+// rt_common.h -- types shared by the render kernels (rt_kernel.hip, rt_wave.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "rt_abi.h"
+#include "rt_math.h"
+
+namespace rtk {
+
+constexpr int TILE = 16;   // shard / tile granularity (16x16 pixels)
+constexpr int BLOCK = 256; // threads of the tile-shaped helper kernels
+constexpr int WAVE = 64;
+
+// Leaf-ordered triangle record (product-side mirror of the reference arrays, built by
+// Scene::Upload): A = (v0.xyz, e1.x), B = (e1.yz, e2.xy), C = (e2.z, face id, 0, 0) with
+// e1 = v1 - v0 and e2 = v2 - v0 computed exactly as glm::intersectRayTriangle does
+// (gtx/intersect.inl:37-38), so the test below is bit-identical to the reference's.
+struct FlatTri {
+    float4 a, b, c;
+};
+
+struct RenderArgs {
+    const GeometrySphere* spheres;
+    const GPUMaterial* materials;
+    const GPUBVHNode* nodes;
+    const uint32_t* face_indices;
+    const GPUVertex* vertices;
+    const GPUFace* faces;
+    const FlatTri* tris;  // null -> reference-layout tracer
+    rt_rng_state* rng;
+    const float* sky;  // float4 [6][n][n] or null
+    int sky_n;
+    int sphere_count;
+    GPUCamera cam;
+    float qw, qx, qy, qz;  // quat(vec3(0, PI, 0)) for the sky lookup (main_raytracing.cu:151)
+    char* surface;
+    const char* last;
+    float4* out_shard;
+    uint64_t pitch;
+    int width, height, frame_index, spp, bounces;
+    int shard_index, shard_count, tiles_x;
+    unsigned long long* stats;
+    unsigned long long* seg_counter;
+    int scene_fast;  // all node bounds inside the filtered-slab range (rt_fast.h)
+};
+
+struct Counters {
+    unsigned long long seg = 0, node = 0, tri = 0, tacc = 0, sacc = 0, hit = 0, miss = 0;
+    unsigned long long w_small = 0, l_small = 0, w_big = 0, l_big = 0, w_seg = 0, l_seg = 0;
+};
+
+__device__ __forceinline__ rtm::f3 ld3(const float* p) { return rtm::f3{p[0], p[1], p[2]}; }
+
+// Tile-local pixel of tile-thread `tid` (0..255): wave w covers the 8x8 sub-tile
+// ((w&1)*8, (w>>1)*8), lane l the pixel (l&7, l>>3) of it.  The compact shard layout and
+// unshard_kernel use the same map.
+__device__ __forceinline__ void tile_pixel(int tid, int* lx, int* ly) {
+    const int w = tid >> 6, l = tid & 63;
+    *lx = (w & 1) * 8 + (l & 7);
+    *ly = (w >> 1) * 8 + (l >> 3);
+}
+
+}  // namespace rtk

@@ -25,7 +25,9 @@
 #include "rt_device.h"
 #include "rt_math.h"
 #include "xorwow.h"
+#include "rt_common.h"
 #include "rt_fast.h"
+#include "rt_wave.h"
 
 bool rt_internal_lookup_mirror(const GPUScene* scene, const void** tris, int* depth, bool* scene_fast);
 
@@ -104,65 +106,8 @@ static int cube_size(uint64_t handle) {
 // ---------------------------------------------------------------------------------------
 namespace {
 
-constexpr int TILE = 16;   // shard / tile granularity (16x16 pixels)
-constexpr int BLOCK = 256; // threads of the tile-shaped helper kernels
-constexpr int WAVE = 64;
-
-// Leaf-ordered triangle record (product-side mirror of the reference arrays, built by
-// Scene::Upload): A = (v0.xyz, e1.x), B = (e1.yz, e2.xy), C = (e2.z, face id, 0, 0) with
-// e1 = v1 - v0 and e2 = v2 - v0 computed exactly as glm::intersectRayTriangle does
-// (gtx/intersect.inl:37-38), so the test below is bit-identical to the reference's.
-struct FlatTri {
-    float4 a, b, c;
-};
-
-struct RenderArgs {
-    const GeometrySphere* spheres;
-    const GPUMaterial* materials;
-    const GPUBVHNode* nodes;
-    const uint32_t* face_indices;
-    const GPUVertex* vertices;
-    const GPUFace* faces;
-    const FlatTri* tris;  // null -> reference-layout tracer
-    rt_rng_state* rng;
-    const float* sky;  // float4 [6][n][n] or null
-    int sky_n;
-    int sphere_count;
-    GPUCamera cam;
-    float qw, qx, qy, qz;  // quat(vec3(0, PI, 0)) for the sky lookup (main_raytracing.cu:151)
-    char* surface;
-    const char* last;
-    float4* out_shard;
-    uint64_t pitch;
-    int width, height, frame_index, spp, bounces;
-    int shard_index, shard_count, tiles_x;
-    unsigned long long* stats;
-    unsigned long long* seg_counter;
-    int scene_fast;  // all node bounds inside the filtered-slab range (rt_fast.h)
-};
-
-struct Counters {
-    unsigned long long seg = 0, node = 0, tri = 0, tacc = 0, sacc = 0, hit = 0, miss = 0;
-    unsigned long long w_small = 0, l_small = 0, w_big = 0, l_big = 0, w_seg = 0, l_seg = 0;
-};
-
-struct Hit {
-    float best;
-    int kind;  // 0 none, 1 sphere, 2 triangle
-    uint32_t id;  // sphere index or face index
-    float bx, by;
-};
-
-__device__ __forceinline__ rtm::f3 ld3(const float* p) { return rtm::f3{p[0], p[1], p[2]}; }
-
-// Tile-local pixel of tile-thread `tid` (0..255): wave w covers the 8x8 sub-tile
-// ((w&1)*8, (w>>1)*8), lane l the pixel (l&7, l>>3) of it.  The compact shard layout and
-// unshard_kernel use the same map.
-__device__ __forceinline__ void tile_pixel(int tid, int* lx, int* ly) {
-    const int w = tid >> 6, l = tid & 63;
-    *lx = (w & 1) * 8 + (l & 7);
-    *ly = (w >> 1) * 8 + (l >> 3);
-}
+using namespace rtk;
+using rtfast::Hit;
 
 // The sphere loop of GetRayHit (main_raytracing.cu:88-103): strict `<` replaces.
 template <bool STATS>
@@ -860,17 +805,20 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     a.tris = force_ref ? nullptr : (const FlatTri*)tris;
     const bool stats = (p->flags & RT_RENDER_STATS) != 0;
     hipStream_t s = (hipStream_t)stream;
-    static const char* which = std::getenv("RT_TRACER");  // A/B switch: ref | flat | fast (default)
+    static const char* which = std::getenv("RT_TRACER");  // A/B switch: ref | flat | mega | wave (default)
     const bool want_flat = (p->flags & RT_RENDER_TRACER_FLAT) || (which && std::strcmp(which, "flat") == 0);
     if ((p->flags & RT_RENDER_TRACER_REF) || (which && std::strcmp(which, "ref") == 0)) a.tris = nullptr;
     a.scene_fast = scene_fast ? 1 : 0;
     hipError_t e;
+    const bool want_mega = (p->flags & RT_RENDER_TRACER_MEGA) || (which && std::strcmp(which, "mega") == 0);
     if (!a.tris)
         e = launch_variant<RefTracer>(a, tiles * 4, depth, stats, s);
     else if (want_flat)
         e = launch_variant<FlatTracer>(a, tiles * 4, depth, stats, s);
-    else
+    else if (want_mega)
         e = launch_fast(a, tiles * 4, depth, stats, s);
+    else
+        e = rt_wave_render(a, tiles, depth, stats, s);
     return check(e, "render_kernel launch");
 }
 
