@@ -27,7 +27,7 @@
 #include "xorwow.h"
 #include "rt_common.h"
 #include "rt_fast.h"
-#include "rt_wave.h"
+#include "rt_persist.h"
 
 bool rt_internal_lookup_mirror(const GPUScene* scene, const void** tris, int* depth, bool* scene_fast);
 
@@ -805,7 +805,7 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     a.tris = force_ref ? nullptr : (const FlatTri*)tris;
     const bool stats = (p->flags & RT_RENDER_STATS) != 0;
     hipStream_t s = (hipStream_t)stream;
-    static const char* which = std::getenv("RT_TRACER");  // A/B switch: ref | flat | mega | wave (default)
+    static const char* which = std::getenv("RT_TRACER");  // A/B switch: ref | flat | mega | persistent (default)
     const bool want_flat = (p->flags & RT_RENDER_TRACER_FLAT) || (which && std::strcmp(which, "flat") == 0);
     if ((p->flags & RT_RENDER_TRACER_REF) || (which && std::strcmp(which, "ref") == 0)) a.tris = nullptr;
     a.scene_fast = scene_fast ? 1 : 0;
@@ -818,7 +818,7 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     else if (want_mega)
         e = launch_fast(a, tiles * 4, depth, stats, s);
     else
-        e = rt_wave_render(a, tiles, depth, stats, s);
+        e = rt_persistent_render(a, tiles, depth, stats, s);
     return check(e, "render_kernel launch");
 }
 
