@@ -25,7 +25,7 @@ LIB_PATH = os.path.join(PKG_DIR, "librt_hip.so")
 ASSETS_DIR = os.path.join(ROOT_DIR, "assets")
 
 RT_RENDER_STATS = 1
-TRACERS = {"persistent": 0, "ref": 2, "flat": 4, "mega": 8}  # rt_render_params.flags
+TRACERS = {"fast": 0, "ref": 2, "flat": 4}  # rt_render_params.flags
 STAT_NAMES = ("segments", "nodes", "tri_tests", "tri_accepts", "sphere_accepts", "hits", "misses", "",
               "wave_small_iters", "lane_small", "wave_big_tris", "lane_big_tris", "wave_segment_iters",
               "lane_segments")
@@ -261,7 +261,7 @@ def init_rng_states(rng, width, height, seed, shard_index=0, shard_count=1, stre
 
 
 def render(scene, surface, last, width, height, spp, bounces, frame_index=0, shard_index=0, shard_count=1,
-           out_shard=None, stats=None, segment_counter=None, stream=None, tracer="persistent"):
+           out_shard=None, stats=None, segment_counter=None, stream=None, tracer="fast"):
     """rt_render: one frame (or one shard of it) on `stream` (default: torch's current stream)."""
     p = RenderParams()
     p.surface = surface.data_ptr() if surface is not None else None

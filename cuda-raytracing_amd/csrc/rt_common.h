@@ -43,6 +43,8 @@ struct RenderArgs {
     unsigned long long* stats;
     unsigned long long* seg_counter;
     int scene_fast;  // all node bounds inside the filtered-slab range (rt_fast.h)
+    uint32_t hot_first, hot_count;  // the scene's largest leaf (kept in LDS by each workgroup)
+    uint32_t tune;  // A/B knobs (RT_TUNE): bit0 no cooperative leaf rounds
 };
 
 struct Counters {

@@ -232,11 +232,124 @@ __device__ __forceinline__ bool inner_step(const float4* nodes4, uint32_t* stk, 
     return false;
 }
 
+// A leaf kept resident in LDS by the workgroup (the scene's largest leaf; SoA records).
+struct HotLeaf {
+    const float4* a;  // LDS
+    const float4* b;
+    const float4* c;
+    uint32_t first, count;  // count 0: none
+};
+
+// glm::intersectRayTriangle + BVHRayHit's accept test (`!(t >= best || t < 0)`) for one
+// candidate; returns whether it would be accepted against threshold `best`, and reports a
+// NaN distance of an otherwise accepted triangle (the sequential reference accepts a NaN t;
+// a min-reduction would not, so such a ray is redone sequentially).
+__device__ __forceinline__ bool tri_accept(f3 o, f3 nd, float4 A, float4 B, float4 Cc, float best, float* t_o,
+                                           float* bx, float* by, bool* nan) {
+    const float eps = 1.1920928955078125e-07f;
+    const f3 e1 = rtm::mk(A.w, B.x, B.y), e2 = rtm::mk(B.z, B.w, Cc.x);
+    const f3 p = rtm::cross(nd, e2);
+    const float det = rtm::dot(e1, p);
+    const f3 dist = rtm::sub(o, rtm::mk(A.x, A.y, A.z));
+    const float u = rtm::dot(dist, p);
+    const f3 perp = rtm::cross(dist, e1);
+    const float v = rtm::dot(nd, perp);
+    const float uv = u + v;
+    const uint32_t sgn = __float_as_uint(det) & 0x80000000u;
+    const float adet = fabsf(det);
+    const float su = __uint_as_float(__float_as_uint(u) ^ sgn);
+    const float sv = __uint_as_float(__float_as_uint(v) ^ sgn);
+    const float suv = __uint_as_float(__float_as_uint(uv) ^ sgn);
+    const bool ok = adet > eps && !(su < 0.0f || su > adet) && !(sv < 0.0f || suv > adet);
+    if (!ok) return false;
+    const float inv_det = 1.0f / det;
+    const float t = rtm::dot(e2, perp) * inv_det;
+    *nan = *nan || (t != t);
+    if (t >= best || t < 0.0f) return false;
+    *t_o = t;
+    *bx = u * inv_det;
+    *by = v * inv_det;
+    return true;
+}
+
+__device__ __forceinline__ float bcast(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// Cooperative big-leaf round: the waiting lanes (mask `big`) all wait at leaf [f0, f0+c0).
+// Rays are taken one at a time; the 64 lanes split the leaf's triangles (lane l tests
+// l, l+64, ...), each keeping its first strictly-closer candidate, and a (t, index)
+// lexicographic arg-min over the wave gives exactly the triangle the sequential loop
+// would end on (the first index attaining the minimum t below the ray's closest distance).
+template <class C>
+__device__ __forceinline__ void coop_leaf(const float4* tris, const HotLeaf& hot, unsigned long long big, uint32_t f0,
+                                          uint32_t c0, const Ray& R, Hit& h, C& c) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool resident = hot.count != 0 && f0 == hot.first && c0 == hot.count;
+    unsigned long long m = big;
+    while (m) {
+        const int r = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const f3 rox = rtm::mk(bcast(R.o.x, r), bcast(R.o.y, r), bcast(R.o.z, r));
+        const f3 nd = rtm::mk(bcast(R.nd.x, r), bcast(R.nd.y, r), bcast(R.nd.z, r));
+        const float best0 = bcast(h.best, r);
+        float bt = best0, bx = 0.0f, by = 0.0f;
+        uint32_t bi = 0xffffffffu;
+        bool nan = false;
+        for (uint32_t j = lane; j < c0; j += 64u) {
+            float4 A, B, Cc;
+            if (resident) {
+                A = hot.a[j], B = hot.b[j], Cc = hot.c[j];
+            } else {
+                A = tris[3 * (f0 + j)], B = tris[3 * (f0 + j) + 1], Cc = tris[3 * (f0 + j) + 2];
+            }
+            float t, x, y;
+            if (tri_accept(rox, nd, A, B, Cc, bt, &t, &x, &y, &nan)) bt = t, bx = x, by = y, bi = j;
+        }
+        if (__ballot(nan)) {
+            // sequential fallback for this ray (never taken for finite scenes)
+            if ((int)lane == r) {
+                float t, x, y;
+                bool dummy = false;
+                for (uint32_t j = 0; j < c0; j++) {
+                    const float4 A = tris[3 * (f0 + j)], B = tris[3 * (f0 + j) + 1], Cc = tris[3 * (f0 + j) + 2];
+                    if (tri_accept(R.o, R.nd, A, B, Cc, h.best, &t, &x, &y, &dummy)) {
+                        h.best = t, h.kind = 2, h.bx = x, h.by = y;
+                        h.id = __float_as_uint(Cc.y);
+                    }
+                }
+            }
+            continue;
+        }
+        // arg-min of (t, index) across the wave
+        float mt = bt;
+        uint32_t mi = bi;
+        for (int off = 32; off > 0; off >>= 1) {
+            const float ot = __shfl_xor(mt, off);
+            const uint32_t oi = (uint32_t)__shfl_xor((int)mi, off);
+            const bool take = ot < mt || (ot == mt && oi < mi);
+            mt = take ? ot : mt;
+            mi = take ? oi : mi;
+        }
+        mi = __builtin_amdgcn_readfirstlane(mi);
+        if (mi != 0xffffffffu) {
+            const int wl = (int)(mi & 63u);
+            const float wbx = bcast(bx, wl), wby = bcast(by, wl), wt = bcast(bt, wl);
+            if ((int)lane == r) {
+                const float4 Cc = resident ? hot.c[mi] : tris[3 * (f0 + mi) + 2];
+                h.best = wt, h.kind = 2, h.bx = wbx, h.by = wby;
+                h.id = __float_as_uint(Cc.y);
+            }
+        }
+    }
+    (void)c;
+}
+
 // BVHRayHit for one lane (`live` = the lane has a segment to trace).  Every lane of the wave
-// must call it (it synchronises big leaves across the wave).
-template <int WAVE, bool STATS, class C>
-__device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, uint32_t* stk, const Ray& R, Hit& h,
-                                      bool live, C& c) {
+// must call it (it synchronises big leaves across the wave).  STRIDE: the stack's lane stride.
+template <int STRIDE, bool STATS, class C>
+__device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, const HotLeaf& hot, bool coop, uint32_t* stk,
+                                      const Ray& R, Hit& h, bool live, C& c) {
     bool active = false;
     uint32_t first = 0, count = 0;
     int sp = 0;
@@ -253,16 +366,16 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
         const bool small = active && count <= (uint32_t)BIG;
         if (__ballot(small)) {
             if (STATS) {
-                c.w_small += threadIdx.x == 0;
+                c.w_small += (threadIdx.x & 63) == 0;
                 c.l_small += small;
             }
             if (small) {
                 if (count > 0) {
                     for (uint32_t i = first; i < first + count; i++)
                         test_triangle<STATS>(R, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], h, c);
-                    active = pop<WAVE>(nodes4, stk, sp, R, h.best, first, count);
-                } else if (!inner_step<WAVE, STATS>(nodes4, stk, sp, R, h.best, first, count, c)) {
-                    active = pop<WAVE>(nodes4, stk, sp, R, h.best, first, count);
+                    active = pop<STRIDE>(nodes4, stk, sp, R, h.best, first, count);
+                } else if (!inner_step<STRIDE, STATS>(nodes4, stk, sp, R, h.best, first, count, c)) {
+                    active = pop<STRIDE>(nodes4, stk, sp, R, h.best, first, count);
                 }
             }
             continue;
@@ -277,25 +390,37 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
         if (STATS) {
             uint32_t mx = active ? count : 0u;
             for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
-            c.w_big += threadIdx.x == 0 ? mx : 0;
+            c.w_big += (threadIdx.x & 63) == 0 ? mx : 0;
             c.l_big += active ? count : 0;
         }
         if (__ballot(active && first == f0) == big) {
-            // all waiting lanes share one leaf: scalar loads, next record prefetched
-            ConstF4 st = (ConstF4)(tris + 3 * (size_t)f0);
-            ConstF4 const last = st + 3 * (c0 - 1);
-            float4 A = ldc(st, 0), B = ldc(st, 1), Cc = ldc(st, 2);
-            for (uint32_t i = 0; i < c0; i++) {
-                st = st == last ? st : st + 3;
-                const float4 An = ldc(st, 0), Bn = ldc(st, 1), Cn = ldc(st, 2);
-                if (active) test_triangle<STATS>(R, A, B, Cc, h, c);
-                A = An, B = Bn, Cc = Cn;
+            const uint32_t k = (uint32_t)__popcll(big);
+            const uint32_t chunks = (c0 + 63u) / 64u;
+            // cost model (VALU instructions): cooperative ~ k * (60 * chunks + 50), lane-parallel ~ 50 * c0
+            if (!STATS && coop && k * (60u * chunks + 50u) < 50u * c0) {
+                coop_leaf(tris, hot, big, f0, c0, R, h, c);
+            } else if (hot.count != 0 && f0 == hot.first && c0 == hot.count) {
+                for (uint32_t i = 0; i < c0; i++) {
+                    const float4 A = hot.a[i], B = hot.b[i], Cc = hot.c[i];
+                    if (active) test_triangle<STATS>(R, A, B, Cc, h, c);
+                }
+            } else {
+                // all waiting lanes share one leaf: scalar loads, next record prefetched
+                ConstF4 st = (ConstF4)(tris + 3 * (size_t)f0);
+                ConstF4 const last = st + 3 * (c0 - 1);
+                float4 A = ldc(st, 0), B = ldc(st, 1), Cc = ldc(st, 2);
+                for (uint32_t i = 0; i < c0; i++) {
+                    st = st == last ? st : st + 3;
+                    const float4 An = ldc(st, 0), Bn = ldc(st, 1), Cn = ldc(st, 2);
+                    if (active) test_triangle<STATS>(R, A, B, Cc, h, c);
+                    A = An, B = Bn, Cc = Cn;
+                }
             }
         } else if (active) {
             for (uint32_t i = first; i < first + count; i++)
                 test_triangle<STATS>(R, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], h, c);
         }
-        if (active) active = pop<WAVE>(nodes4, stk, sp, R, h.best, first, count);
+        if (active) active = pop<STRIDE>(nodes4, stk, sp, R, h.best, first, count);
     }
 }
 

@@ -27,9 +27,9 @@
 #include "xorwow.h"
 #include "rt_common.h"
 #include "rt_fast.h"
-#include "rt_persist.h"
 
-bool rt_internal_lookup_mirror(const GPUScene* scene, const void** tris, int* depth, bool* scene_fast);
+bool rt_internal_lookup_mirror(const GPUScene* scene, const void** tris, int* depth, bool* scene_fast,
+                               uint32_t* hot_first, uint32_t* hot_count);
 
 // ---------------------------------------------------------------------------------------
 // error state
@@ -427,15 +427,30 @@ __global__ __launch_bounds__(WAVE) void render_kernel(RenderArgs a) {
 // start a camera sample, trace a segment, shade, end the path on a miss / Russian roulette /
 // the bounce limit, start its next sample -- so a lane only idles once its whole pixel is
 // done.  The per-pixel draw order (u, v, then 4 draws per hit) is the reference's.
-template <int STACK, bool STATS>
-__global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
-    __shared__ uint32_t stack_lds[STACK * 2 * WAVE];
-    uint32_t* const stk = stack_lds + threadIdx.x;
+template <int STACK, bool STATS, int WG>
+__global__ __launch_bounds__(WG) void render_fast_kernel(RenderArgs a) {
+    // dynamic LDS: [hot leaf SoA: 3 x hot_count float4 (WG == BLOCK only)][stack: STACK x 2 x WG words]
+    extern __shared__ __attribute__((aligned(16))) char smem[];
     const float4* nodes4 = reinterpret_cast<const float4*>(a.nodes);
     const float4* tris = reinterpret_cast<const float4*>(a.tris);
-    const int g = (int)blockIdx.x;
-    const int k = g >> 2;
-    const int tid = ((g & 3) << 6) | (int)threadIdx.x;
+    const uint32_t hot_count = WG == BLOCK ? a.hot_count : 0u;
+    float4* const hot_lds = reinterpret_cast<float4*>(smem);
+    uint32_t* const stk = reinterpret_cast<uint32_t*>(smem + 48 * (size_t)hot_count) + threadIdx.x;
+    if (WG == BLOCK) {
+        for (uint32_t i = threadIdx.x; i < hot_count; i += BLOCK) {
+            const size_t t = 3 * ((size_t)a.hot_first + i);
+            hot_lds[i] = tris[t];
+            hot_lds[hot_count + i] = tris[t + 1];
+            hot_lds[2 * hot_count + i] = tris[t + 2];
+        }
+        __syncthreads();
+    }
+    rtfast::HotLeaf hot;
+    hot.a = hot_lds, hot.b = hot_lds + hot_count, hot.c = hot_lds + 2 * hot_count;
+    hot.first = a.hot_first, hot.count = hot_count;
+    // WG == BLOCK: one workgroup per 16x16 tile; WG == WAVE: one per 8x8 sub-tile
+    const int k = WG == BLOCK ? (int)blockIdx.x : (int)blockIdx.x >> 2;
+    const int tid = WG == BLOCK ? (int)threadIdx.x : (((int)blockIdx.x & 3) << 6) | (int)threadIdx.x;
     const int tile = a.shard_index + k * a.shard_count;
     int lx, ly;
     tile_pixel(tid, &lx, &ly);
@@ -503,7 +518,7 @@ __global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
         }
         if (!__ballot(path)) break;
         if (STATS) {
-            c.w_seg += threadIdx.x == 0;
+            c.w_seg += (threadIdx.x & 63) == 0;
             c.l_seg += path;
         }
 
@@ -526,7 +541,7 @@ __global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
             }
         }
         const rtfast::Ray R = rtfast::make_ray(ro, rd, nd, scene_fast);
-        rtfast::trace<WAVE, STATS>(nodes4, tris, stk, R, h, path, c);
+        rtfast::trace<WG, STATS>(nodes4, tris, hot, (a.tune & 1u) == 0, stk, R, h, path, c);
         if (!path) continue;
 
         bool end = false;
@@ -598,7 +613,7 @@ __global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
     if (a.seg_counter) {
         unsigned long long v = c.seg;
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if (threadIdx.x == 0) atomicAdd(a.seg_counter, v);
+        if ((threadIdx.x & 63) == 0) atomicAdd(a.seg_counter, v);
     }
     if (STATS) {
         atomicAdd(a.stats + RT_STAT_SEGMENTS, c.seg);
@@ -702,18 +717,33 @@ hipError_t launch(const RenderArgs& args, int waves, hipStream_t stream) {
     return hipGetLastError();
 }
 
-template <int STACK, bool STATS>
-hipError_t launch_fast_t(const RenderArgs& args, int waves, hipStream_t stream) {
-    hipLaunchKernelGGL((render_fast_kernel<STACK, STATS>), dim3(waves), dim3(WAVE), 0, stream, args);
+template <int STACK, bool STATS, int WG>
+hipError_t launch_fast_wg(const RenderArgs& args, int tiles, hipStream_t stream) {
+    const size_t lds = (WG == BLOCK ? 48 * (size_t)args.hot_count : 0) + (size_t)STACK * 2 * WG * 4;
+    static bool attr_set = false;  // allow more than the default 64 KiB of dynamic LDS (160 KiB on gfx950)
+    if (!attr_set) {
+        const hipError_t e = hipFuncSetAttribute((const void*)render_fast_kernel<STACK, STATS, WG>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    const int blocks = WG == BLOCK ? tiles : tiles * 4;
+    hipLaunchKernelGGL((render_fast_kernel<STACK, STATS, WG>), dim3(blocks), dim3(WG), lds, stream, args);
     return hipGetLastError();
 }
 
-hipError_t launch_fast(const RenderArgs& args, int waves, int depth, bool stats, hipStream_t s) {
+template <int STACK, bool STATS>
+hipError_t launch_fast_t(const RenderArgs& args, int tiles, hipStream_t stream) {
+    return (args.tune & 4u) ? launch_fast_wg<STACK, STATS, BLOCK>(args, tiles, stream)
+                            : launch_fast_wg<STACK, STATS, WAVE>(args, tiles, stream);
+}
+
+hipError_t launch_fast(const RenderArgs& args, int tiles, int depth, bool stats, hipStream_t s) {
     if (depth >= 0 && depth + 2 <= 28)
-        return stats ? launch_fast_t<28, true>(args, waves, s) : launch_fast_t<28, false>(args, waves, s);
+        return stats ? launch_fast_t<28, true>(args, tiles, s) : launch_fast_t<28, false>(args, tiles, s);
     if (depth >= 0 && depth + 2 <= 40)
-        return stats ? launch_fast_t<40, true>(args, waves, s) : launch_fast_t<40, false>(args, waves, s);
-    return stats ? launch_fast_t<64, true>(args, waves, s) : launch_fast_t<64, false>(args, waves, s);
+        return stats ? launch_fast_t<40, true>(args, tiles, s) : launch_fast_t<40, false>(args, tiles, s);
+    return stats ? launch_fast_t<64, true>(args, tiles, s) : launch_fast_t<64, false>(args, tiles, s);
 }
 
 template <class Tracer>
@@ -800,25 +830,27 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     const void* tris = nullptr;
     int depth = -1;
     bool scene_fast = false;
-    rt_internal_lookup_mirror(scene, &tris, &depth, &scene_fast);
+    uint32_t hot_first = 0, hot_count = 0;
+    rt_internal_lookup_mirror(scene, &tris, &depth, &scene_fast, &hot_first, &hot_count);
+    static const char* tune = std::getenv("RT_TUNE");  // A/B knobs: bit0 no coop rounds, bit1 no LDS hot leaf, bit2 256-thread tiles
+    a.tune = tune ? (uint32_t)std::strtoul(tune, nullptr, 0) : 0u;
+    a.hot_first = hot_first;
+    a.hot_count = (a.tune & 2u) ? 0u : hot_count;
     static const bool force_ref = std::getenv("RT_FORCE_REFERENCE_LAYOUT") != nullptr;  // A/B switch
     a.tris = force_ref ? nullptr : (const FlatTri*)tris;
     const bool stats = (p->flags & RT_RENDER_STATS) != 0;
     hipStream_t s = (hipStream_t)stream;
-    static const char* which = std::getenv("RT_TRACER");  // A/B switch: ref | flat | mega | persistent (default)
+    static const char* which = std::getenv("RT_TRACER");  // A/B switch: ref | flat | fast (default)
     const bool want_flat = (p->flags & RT_RENDER_TRACER_FLAT) || (which && std::strcmp(which, "flat") == 0);
     if ((p->flags & RT_RENDER_TRACER_REF) || (which && std::strcmp(which, "ref") == 0)) a.tris = nullptr;
     a.scene_fast = scene_fast ? 1 : 0;
     hipError_t e;
-    const bool want_mega = (p->flags & RT_RENDER_TRACER_MEGA) || (which && std::strcmp(which, "mega") == 0);
     if (!a.tris)
         e = launch_variant<RefTracer>(a, tiles * 4, depth, stats, s);
     else if (want_flat)
         e = launch_variant<FlatTracer>(a, tiles * 4, depth, stats, s);
-    else if (want_mega)
-        e = launch_fast(a, tiles * 4, depth, stats, s);
     else
-        e = rt_persistent_render(a, tiles, depth, stats, s);
+        e = launch_fast(a, tiles, depth, stats, s);
     return check(e, "render_kernel launch");
 }
 

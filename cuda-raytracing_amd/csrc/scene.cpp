@@ -20,14 +20,17 @@ struct Mirror {
     const void* tris;
     int depth;
     bool fast;
+    uint32_t hot_first, hot_count;
 };
 std::mutex g_mirror_mutex;
 std::map<const void*, Mirror> g_mirrors;  // keyed by the device BVH node array
 }  // namespace
 
-void rt_internal_register_mirror(const GPUScene* s, const void* tris, int depth, bool fast) {
+void rt_internal_register_mirror(const GPUScene* s, const void* tris, int depth, bool fast, uint32_t hot_first,
+                                 uint32_t hot_count) {
     std::lock_guard<std::mutex> lock(g_mirror_mutex);
-    g_mirrors[s->gpu_bvh_nodes] = Mirror{s->gpu_bvh_face_indices, s->gpu_vertices, s->gpu_faces, tris, depth, fast};
+    g_mirrors[s->gpu_bvh_nodes] =
+        Mirror{s->gpu_bvh_face_indices, s->gpu_vertices, s->gpu_faces, tris, depth, fast, hot_first, hot_count};
 }
 void rt_internal_forget_mirror(const void* gpu_nodes) {
     std::lock_guard<std::mutex> lock(g_mirror_mutex);
@@ -35,16 +38,20 @@ void rt_internal_forget_mirror(const void* gpu_nodes) {
 }
 // The leaf-ordered triangle mirror is used only while ALL the reference arrays it was built
 // from are still the ones the GPUScene points at.
-bool rt_internal_lookup_mirror(const GPUScene* s, const void** tris, int* depth, bool* fast) {
+bool rt_internal_lookup_mirror(const GPUScene* s, const void** tris, int* depth, bool* fast, uint32_t* hot_first,
+                               uint32_t* hot_count) {
     std::lock_guard<std::mutex> lock(g_mirror_mutex);
     auto it = g_mirrors.find(s->gpu_bvh_nodes);
     *tris = nullptr;
     *depth = -1;
     *fast = false;
+    *hot_first = *hot_count = 0;
     if (it == g_mirrors.end()) return false;
     const Mirror& m = it->second;
     *depth = m.depth;
     *fast = m.fast;
+    *hot_first = m.hot_first;
+    *hot_count = m.hot_count;
     if (m.face_indices != s->gpu_bvh_face_indices || m.vertices != s->gpu_vertices || m.faces != s->gpu_faces)
         return false;
     *tris = m.tris;
@@ -409,7 +416,13 @@ void Scene::Upload(void* rng) {
                 if ((lo != 0.0f && (lo < 0x1p-60f || lo > 0x1p62f)) || (hi != 0.0f && (hi < 0x1p-60f || hi > 0x1p62f)))
                     fast = false;
             }
-        rt_internal_register_mirror(this, tris_memory->GetMemory(), bvh->GetMaxDepth(), fast);
+        // The largest leaf stays resident in each workgroup's LDS (kernel rtfast::HotLeaf) when it
+        // is big enough to matter and small enough to fit (the bunny scene's floor leaf: 345).
+        uint32_t hot_first = 0, hot_count = 0;
+        for (size_t n = 0; n < bvh->GetNodeCount(); n++)
+            if (bn[n].prim_count > hot_count) hot_count = bn[n].prim_count, hot_first = bn[n].first_index;
+        if (hot_count <= 8 || hot_count > 512) hot_first = hot_count = 0;
+        rt_internal_register_mirror(this, tris_memory->GetMemory(), bvh->GetMaxDepth(), fast, hot_first, hot_count);
         tris_pending = false;
     }
     dirty_flags = 0;

@@ -153,6 +153,8 @@ void SetupPlaneGrid(Scene& scene, int n);
 
 // Leaf-ordered triangle mirror + BVH depth registered by Scene::Upload for the device
 // arrays of a GPUScene (kernel fast path and stack sizing; see rt_kernel.hip).
-void rt_internal_register_mirror(const GPUScene* scene, const void* tris, int depth, bool fast);
+void rt_internal_register_mirror(const GPUScene* scene, const void* tris, int depth, bool fast, uint32_t hot_first,
+                                 uint32_t hot_count);
 void rt_internal_forget_mirror(const void* gpu_nodes);
-bool rt_internal_lookup_mirror(const GPUScene* scene, const void** tris, int* depth, bool* fast);
+bool rt_internal_lookup_mirror(const GPUScene* scene, const void** tris, int* depth, bool* fast, uint32_t* hot_first,
+                               uint32_t* hot_count);

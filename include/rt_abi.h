@@ -171,7 +171,6 @@ typedef struct rt_render_params {
 #define RT_RENDER_STATS 1          /* count traversal work (slower kernel variant) */
 #define RT_RENDER_TRACER_REF 2     /* force the reference-layout tracer (A/B, tests) */
 #define RT_RENDER_TRACER_FLAT 4    /* force the exact-division flat tracer (A/B, tests) */
-#define RT_RENDER_TRACER_MEGA 8    /* force the per-pixel fast megakernel (A/B, tests) */
 
 enum {
     RT_STAT_SEGMENTS = 0,   /* GetRayHit calls */

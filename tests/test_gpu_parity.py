@@ -31,7 +31,7 @@ def make_scene(rt, which, w, h, plane_n=None):
     return s
 
 
-def gpu_render(rt, which, w, h, spp, bounces, frames=1, plane_n=None, seed=T.SEED, stats=False, tracer="persistent"):
+def gpu_render(rt, which, w, h, spp, bounces, frames=1, plane_n=None, seed=T.SEED, stats=False, tracer="fast"):
     s = make_scene(rt, which, w, h, plane_n)
     rng = rt.alloc_rng(w * h)
     rt.init_rng_states(rng, w, h, seed)
@@ -89,7 +89,7 @@ def test_init_rng_reference_entry_point(rt):
         assert np.array_equal(got[i], T.oracle_rng_state(12345, i)), i
 
 
-@pytest.mark.parametrize("tracer", ["persistent", "mega", "flat", "ref"])
+@pytest.mark.parametrize("tracer", ["fast", "flat", "ref"])
 @pytest.mark.parametrize("spp,bounces", [(1, 1), (4, 6), (8, 6)])
 def test_render_bunny_small(rt, spp, bounces, tracer):
     """Every kernel variant (production fast path, exact-division flat path, reference-layout
@@ -175,11 +175,11 @@ def test_tracers_agree_medium(rt, which, plane_n):
     """256x144, 4 spp, 6 bounces: the three kernel variants produce identical frames and RNG
     states (a larger sample of rays than the oracle comparisons above)."""
     res = {t: gpu_render(rt, which, 256, 144, 4, 6, plane_n=plane_n, stats=True, tracer=t)
-           for t in ("persistent", "mega", "flat", "ref")}
-    for t in ("mega", "flat", "ref"):
-        assert np.array_equal(res["persistent"]["frames"][0], res[t]["frames"][0]), t
-        assert np.array_equal(res["persistent"]["rng"], res[t]["rng"]), t
-        assert np.array_equal(res["persistent"]["stats"][:7], res[t]["stats"][:7]), t
+           for t in ("fast", "flat", "ref")}
+    for t in ("flat", "ref"):
+        assert np.array_equal(res["fast"]["frames"][0], res[t]["frames"][0]), t
+        assert np.array_equal(res["fast"]["rng"], res[t]["rng"]), t
+        assert np.array_equal(res["fast"]["stats"][:7], res[t]["stats"][:7]), t
 
 
 def test_full_size_config2_properties(rt):
