@@ -231,7 +231,7 @@ def main():
                        "segments_per_step": round(segs_total / args.steps, 1)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config),
-                         "kernel": "render_kernel", "kernel_ms": round(kern_avg_s * 1e3, 3),
+                         "kernel": "render_fast_kernel", "kernel_ms": round(kern_avg_s * 1e3, 3),
                          "algorithmic_bytes_per_launch": int(bytes_per_launch),
                          "frame0_counts": {k: int(v) for k, v in zip(rt.STAT_NAMES, stats0) if k}},
             "setup_s": round(setup_s, 2),

@@ -143,16 +143,38 @@ __device__ __forceinline__ float4 ldc(ConstF4 p, uint32_t i) {
 }
 
 // Pop stack entries until one passes `tmin < closest` (the reference's pop-time test).
-// Entry: word 0 = node index | (tmin is exact) << 31, word 1 = tmin bits.
-template <int WAVE>
+// SW == 2: entry = {node index | (tmin is exact) << 31, tmin bits}.
+// SW == 1: entry = node index; tmin is recomputed from the node (the same slab arithmetic gives
+// the same value, so the decision is the reference's), halving the LDS per lane.
+template <int WAVE, int SW>
 __device__ __forceinline__ bool pop(const float4* nodes4, uint32_t* stk, int& sp, const Ray& R, float best,
                                     uint32_t& first, uint32_t& count) {
     while (sp > 0) {
         sp--;
-        const uint32_t w0 = stk[(sp * 2) * WAVE];
-        const float t = __uint_as_float(stk[(sp * 2 + 1) * WAVE]);
+        const uint32_t w0 = stk[(sp * SW) * WAVE];
         const uint32_t idx = w0 & 0x7fffffffu;
         bool pass;
+        if (SW == 1) {
+            const float4 lo = nodes4[2 * idx], hi = nodes4[2 * idx + 1];
+            int cl = UNSURE;
+            float te, tx;
+            if (R.fast) {
+                slab_approx(R, lo, hi, &te, &tx);
+                cl = classify_lt(te, best);
+            }
+            if (cl == UNSURE) {
+                slab_exact(R, lo, hi, &te, &tx);
+                pass = te < best;
+            } else {
+                pass = cl == YES;
+            }
+            if (pass) {
+                first = __float_as_uint(hi.z), count = __float_as_uint(hi.w);
+                return true;
+            }
+            continue;
+        }
+        const float t = __uint_as_float(stk[(sp * SW + 1) * WAVE]);
         if (w0 >> 31) {
             pass = t < best;
         } else {
@@ -177,7 +199,7 @@ __device__ __forceinline__ bool pop(const float4* nodes4, uint32_t* stk, int& sp
 // One inner-node step: both children (adjacent in the node array) tested, the right child
 // continued in registers, the left one continued or pushed, exactly as the reference's
 // push(first), push(first+1), pop order.  Returns false when the lane must pop.
-template <int WAVE, bool STATS, class C>
+template <int WAVE, int SW, bool STATS, class C>
 __device__ __forceinline__ bool inner_step(const float4* nodes4, uint32_t* stk, int& sp, const Ray& R, float best,
                                            uint32_t& first, uint32_t& count, C& c) {
     const float4 l0 = nodes4[2 * first], l1 = nodes4[2 * first + 1];
@@ -203,8 +225,12 @@ __device__ __forceinline__ bool inner_step(const float4* nodes4, uint32_t* stk, 
     }
     if (rlt == YES) {
         if (okl == YES) {
-            stk[(sp * 2) * WAVE] = first | (exact_l ? 0x80000000u : 0u);
-            stk[(sp * 2 + 1) * WAVE] = __float_as_uint(tl);
+            if (SW == 1) {
+                stk[sp * WAVE] = first;
+            } else {
+                stk[(sp * 2) * WAVE] = first | (exact_l ? 0x80000000u : 0u);
+                stk[(sp * 2 + 1) * WAVE] = __float_as_uint(tl);
+            }
             sp++;
         }
         first = __float_as_uint(r1.z), count = __float_as_uint(r1.w);
@@ -347,7 +373,7 @@ __device__ __forceinline__ void coop_leaf(const float4* tris, const HotLeaf& hot
 
 // BVHRayHit for one lane (`live` = the lane has a segment to trace).  Every lane of the wave
 // must call it (it synchronises big leaves across the wave).  STRIDE: the stack's lane stride.
-template <int STRIDE, bool STATS, class C>
+template <int STRIDE, int SW, bool STATS, class C>
 __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, const HotLeaf& hot, bool coop, uint32_t* stk,
                                       const Ray& R, Hit& h, bool live, C& c) {
     bool active = false;
@@ -373,9 +399,9 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                 if (count > 0) {
                     for (uint32_t i = first; i < first + count; i++)
                         test_triangle<STATS>(R, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], h, c);
-                    active = pop<STRIDE>(nodes4, stk, sp, R, h.best, first, count);
-                } else if (!inner_step<STRIDE, STATS>(nodes4, stk, sp, R, h.best, first, count, c)) {
-                    active = pop<STRIDE>(nodes4, stk, sp, R, h.best, first, count);
+                    active = pop<STRIDE, SW>(nodes4, stk, sp, R, h.best, first, count);
+                } else if (!inner_step<STRIDE, SW, STATS>(nodes4, stk, sp, R, h.best, first, count, c)) {
+                    active = pop<STRIDE, SW>(nodes4, stk, sp, R, h.best, first, count);
                 }
             }
             continue;
@@ -420,7 +446,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
             for (uint32_t i = first; i < first + count; i++)
                 test_triangle<STATS>(R, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], h, c);
         }
-        if (active) active = pop<STRIDE>(nodes4, stk, sp, R, h.best, first, count);
+        if (active) active = pop<STRIDE, SW>(nodes4, stk, sp, R, h.best, first, count);
     }
 }
 

@@ -427,9 +427,9 @@ __global__ __launch_bounds__(WAVE) void render_kernel(RenderArgs a) {
 // start a camera sample, trace a segment, shade, end the path on a miss / Russian roulette /
 // the bounce limit, start its next sample -- so a lane only idles once its whole pixel is
 // done.  The per-pixel draw order (u, v, then 4 draws per hit) is the reference's.
-template <int STACK, bool STATS, int WG>
+template <int STACK, bool STATS, int WG, int SW>
 __global__ __launch_bounds__(WG) void render_fast_kernel(RenderArgs a) {
-    // dynamic LDS: [hot leaf SoA: 3 x hot_count float4 (WG == BLOCK only)][stack: STACK x 2 x WG words]
+    // dynamic LDS: [hot leaf SoA: 3 x hot_count float4 (WG == BLOCK only)][stack: STACK x SW x WG words]
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const float4* nodes4 = reinterpret_cast<const float4*>(a.nodes);
     const float4* tris = reinterpret_cast<const float4*>(a.tris);
@@ -541,7 +541,7 @@ __global__ __launch_bounds__(WG) void render_fast_kernel(RenderArgs a) {
             }
         }
         const rtfast::Ray R = rtfast::make_ray(ro, rd, nd, scene_fast);
-        rtfast::trace<WG, STATS>(nodes4, tris, hot, (a.tune & 1u) == 0, stk, R, h, path, c);
+        rtfast::trace<WG, SW, STATS>(nodes4, tris, hot, (a.tune & 1u) == 0, stk, R, h, path, c);
         if (!path) continue;
 
         bool end = false;
@@ -717,25 +717,26 @@ hipError_t launch(const RenderArgs& args, int waves, hipStream_t stream) {
     return hipGetLastError();
 }
 
-template <int STACK, bool STATS, int WG>
+template <int STACK, bool STATS, int WG, int SW>
 hipError_t launch_fast_wg(const RenderArgs& args, int tiles, hipStream_t stream) {
-    const size_t lds = (WG == BLOCK ? 48 * (size_t)args.hot_count : 0) + (size_t)STACK * 2 * WG * 4;
+    const size_t lds = (WG == BLOCK ? 48 * (size_t)args.hot_count : 0) + (size_t)STACK * SW * WG * 4;
     static bool attr_set = false;  // allow more than the default 64 KiB of dynamic LDS (160 KiB on gfx950)
     if (!attr_set) {
-        const hipError_t e = hipFuncSetAttribute((const void*)render_fast_kernel<STACK, STATS, WG>,
+        const hipError_t e = hipFuncSetAttribute((const void*)render_fast_kernel<STACK, STATS, WG, SW>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     const int blocks = WG == BLOCK ? tiles : tiles * 4;
-    hipLaunchKernelGGL((render_fast_kernel<STACK, STATS, WG>), dim3(blocks), dim3(WG), lds, stream, args);
+    hipLaunchKernelGGL((render_fast_kernel<STACK, STATS, WG, SW>), dim3(blocks), dim3(WG), lds, stream, args);
     return hipGetLastError();
 }
 
 template <int STACK, bool STATS>
 hipError_t launch_fast_t(const RenderArgs& args, int tiles, hipStream_t stream) {
-    return (args.tune & 4u) ? launch_fast_wg<STACK, STATS, BLOCK>(args, tiles, stream)
-                            : launch_fast_wg<STACK, STATS, WAVE>(args, tiles, stream);
+    if (args.tune & 4u) return launch_fast_wg<STACK, STATS, BLOCK, 2>(args, tiles, stream);
+    if (args.tune & 8u) return launch_fast_wg<STACK, STATS, WAVE, 2>(args, tiles, stream);
+    return launch_fast_wg<STACK, STATS, WAVE, 1>(args, tiles, stream);
 }
 
 hipError_t launch_fast(const RenderArgs& args, int tiles, int depth, bool stats, hipStream_t s) {
@@ -832,7 +833,7 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     bool scene_fast = false;
     uint32_t hot_first = 0, hot_count = 0;
     rt_internal_lookup_mirror(scene, &tris, &depth, &scene_fast, &hot_first, &hot_count);
-    static const char* tune = std::getenv("RT_TUNE");  // A/B knobs: bit0 no coop rounds, bit1 no LDS hot leaf, bit2 256-thread tiles
+    static const char* tune = std::getenv("RT_TUNE");  // A/B knobs: bit0 no coop rounds, bit1 no LDS hot leaf, bit2 256-thread tiles, bit3 two-word stack entries
     a.tune = tune ? (uint32_t)std::strtoul(tune, nullptr, 0) : 0u;
     a.hot_first = hot_first;
     a.hot_count = (a.tune & 2u) ? 0u : hot_count;
