@@ -172,7 +172,7 @@ def main():
                       segment_counter=seg_counter if i >= args.warmup else None)
         ev[i][1].record(stream)
         if sharded:
-            dist.gather(cur, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+            rt.sharding.gather_shards(cur, rank, world, out=gathered)
             if rank == 0:
                 rt.unshard(frame, W, H, world, gathered, per_shard)
 

@@ -108,6 +108,8 @@ SIGNATURES = {
     "rt_scene_host_arrays": (_SZ, [_P, ctypes.POINTER(_P), ctypes.POINTER(_SZ), ctypes.POINTER(_P),
                                    ctypes.POINTER(_SZ), ctypes.POINTER(_P), ctypes.POINTER(_SZ), ctypes.POINTER(_P)]),
     "rt_scene_bvh_max_depth": (_I, [_P]),
+    "rt_scene_mirror_info": (_I, [_P, ctypes.POINTER(_SZ)]),
+    "rt_scene_mirror_copy": (_I, [_P, _P]),
     "rt_xorwow_jump_matrix": (_I, [_I, ctypes.POINTER(ctypes.c_uint32)]),
     "rt_xorwow_init_host": (None, [_U32, _U64, _P]),
 }
@@ -220,6 +222,16 @@ class Scene:
     def max_depth(self):
         return lib().rt_scene_bvh_max_depth(self.handle)
 
+    def mirror(self):
+        """The kernel's leaf-ordered triangle mirror built on the host (mirror.h): (N,12) float32
+        records (v0, e1, e2, face id bits, 0, 0)."""
+        import numpy as np
+        n = ctypes.c_size_t()
+        _check(lib().rt_scene_mirror_info(self.handle, ctypes.byref(n)), "rt_scene_mirror_info")
+        tris = np.zeros((n.value, 12), dtype=np.float32)
+        _check(lib().rt_scene_mirror_copy(self.handle, tris.ctypes.data), "rt_scene_mirror_copy")
+        return tris
+
     def host_arrays(self):
         """numpy copies of the host arrays: nodes (N,8) f32/u32 view, face indices, vertices, faces."""
         import numpy as np
@@ -277,7 +289,8 @@ def render(scene, surface, last, width, height, spp, bounces, frame_index=0, sha
     if stats is not None:
         p.flags |= RT_RENDER_STATS
         p.stats = stats.data_ptr()
-    _check(lib().rt_render(ctypes.byref(p), ctypes.cast(scene.gpu, ctypes.c_void_p), _stream_ptr(stream)), "rt_render")
+    gpu = scene.gpu if hasattr(scene, "gpu") else ctypes.pointer(scene)  # Scene, or a GPUScene filled by the caller
+    _check(lib().rt_render(ctypes.byref(p), ctypes.cast(gpu, ctypes.c_void_p), _stream_ptr(stream)), "rt_render")
 
 
 def shard_tiles(width, height, shard_index, shard_count):
@@ -335,3 +348,6 @@ class RayTracer:
         self.last_frame.copy_(self.surface)
         self.frame_index += 1
         return surface_view(self.surface, self.width)
+
+
+from . import sharding  # noqa: E402  (multi-GPU tile bookkeeping; the data path is in librt_hip.so)

@@ -1,0 +1,136 @@
+// mirror.cpp -- host construction and device registry of the kernel's triangle mirror
+// (see mirror.h for the layout).
+#include "mirror.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+
+namespace {
+void put_flat(float* o, const float* p0, const float* p1, const float* p2, uint32_t face) {
+    o[0] = p0[0], o[1] = p0[1], o[2] = p0[2];
+    o[3] = p1[0] - p0[0], o[4] = p1[1] - p0[1], o[5] = p1[2] - p0[2];  // fp32, as glm forms them
+    o[6] = p2[0] - p0[0], o[7] = p2[1] - p0[1], o[8] = p2[2] - p0[2];
+    std::memcpy(&o[9], &face, 4);
+    o[10] = o[11] = 0.0f;
+}
+}  // namespace
+
+void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t* fi, size_t index_count,
+                     const GPUFace* faces, size_t face_count, const GPUVertex* verts, size_t vertex_count,
+                     MirrorHost* out) {
+    auto bad = [](const char* what) { throw std::runtime_error(std::string("mirror: ") + what); };
+    out->tris.assign(index_count * 12, 0.0f);
+    for (size_t i = 0; i < index_count; i++) {
+        const uint32_t f = fi[i];
+        if (f >= face_count) bad("face index out of range");
+        const GPUFace& fc = faces[f];
+        if (fc.v0 >= vertex_count || fc.v1 >= vertex_count || fc.v2 >= vertex_count) bad("vertex index out of range");
+        put_flat(&out->tris[i * 12], verts[fc.v0].position, verts[fc.v1].position, verts[fc.v2].position, f);
+    }
+
+    // walk the tree from the root: depth, filtered-slab range, largest leaf
+    out->depth = 0;
+    out->fast = true;
+    out->hot_first = out->hot_count = 0;
+    if (node_count == 0) return;
+    std::vector<std::pair<uint32_t, int>> st{{0u, 0}};
+    size_t visited = 0;
+    while (!st.empty()) {
+        const auto [n, d] = st.back();
+        st.pop_back();
+        if (n >= node_count) bad("node index out of range");
+        if (++visited > node_count) bad("node graph is not a tree");
+        const GPUBVHNode& nd = nodes[n];
+        for (int k = 0; k < 3; k++) {
+            const float lo = std::fabs(nd.bmin[k]), hi = std::fabs(nd.bmax[k]);
+            if ((lo != 0.0f && (lo < 0x1p-60f || lo > 0x1p62f)) || (hi != 0.0f && (hi < 0x1p-60f || hi > 0x1p62f)))
+                out->fast = false;
+        }
+        if (nd.prim_count > 0) {
+            if ((size_t)nd.first_index + nd.prim_count > index_count) bad("leaf range out of range");
+            out->depth = std::max(out->depth, d);
+            if (nd.prim_count > out->hot_count) out->hot_count = nd.prim_count, out->hot_first = nd.first_index;
+        } else {
+            st.push_back({nd.first_index, d + 1});
+            st.push_back({nd.first_index + 1, d + 1});
+        }
+    }
+    if (out->hot_count <= 8 || out->hot_count > 512) out->hot_first = out->hot_count = 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// registry
+// ---------------------------------------------------------------------------------------
+namespace {
+struct Entry {
+    const void* face_indices;
+    const void* vertices;
+    const void* faces;
+    void* block;  // device copy of the tris records
+    MirrorDevice dev;
+};
+std::mutex g_mutex;
+std::map<const void*, Entry> g_mirrors;  // keyed by the device BVH node array
+
+void release(Entry& e) {
+    if (e.block) rt_free(e.block);
+    e.block = nullptr;
+}
+}  // namespace
+
+int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owned, uint64_t fingerprint) {
+    const size_t nt = m.tris.size() * 4;
+    void* block = nullptr;
+    if (rt_malloc(&block, nt + 64) != 0) return -1;
+    char* b = static_cast<char*>(block);
+    if (nt && rt_memcpy_h2d(b, m.tris.data(), nt) != 0) {
+        rt_free(block);
+        return -1;
+    }
+    Entry e{s->gpu_bvh_face_indices, s->gpu_vertices, s->gpu_faces, block, {}};
+    e.dev.tris = b;
+    e.dev.depth = m.depth;
+    e.dev.fast = m.fast;
+    e.dev.hot_first = m.hot_first;
+    e.dev.hot_count = m.hot_count;
+    e.dev.owned = owned;
+    e.dev.fingerprint = fingerprint;
+    std::lock_guard<std::mutex> lock(g_mutex);
+    auto it = g_mirrors.find(s->gpu_bvh_nodes);
+    if (it != g_mirrors.end()) {
+        release(it->second);
+        g_mirrors.erase(it);
+    }
+    g_mirrors.emplace(s->gpu_bvh_nodes, e);
+    return 0;
+}
+
+void rt_internal_forget_mirror(const void* gpu_nodes) {
+    std::lock_guard<std::mutex> lock(g_mutex);
+    auto it = g_mirrors.find(gpu_nodes);
+    if (it == g_mirrors.end()) return;
+    release(it->second);
+    g_mirrors.erase(it);
+}
+
+// The mirror is used only while ALL the reference arrays it was built from are still the
+// ones the GPUScene points at (and, for a foreign scene, the caller checks the fingerprint);
+// otherwise only the depth (stack sizing) is reported.
+bool rt_internal_lookup_mirror(const GPUScene* s, MirrorDevice* out) {
+    std::lock_guard<std::mutex> lock(g_mutex);
+    *out = MirrorDevice{};
+    auto it = g_mirrors.find(s->gpu_bvh_nodes);
+    if (it == g_mirrors.end()) return false;
+    const Entry& e = it->second;
+    if (e.face_indices != s->gpu_bvh_face_indices || e.vertices != s->gpu_vertices || e.faces != s->gpu_faces) {
+        out->depth = e.dev.depth;
+        return false;
+    }
+    *out = e.dev;
+    return true;
+}

@@ -1,0 +1,50 @@
+// mirror.h -- the render kernel's private, read-only view of a GPUScene's triangles.
+//
+// The reference arrays (GPUBVHNode / face_indices / GPUFace / GPUVertex, GPUScene.h:25-74)
+// stay authoritative; from them the host derives once per geometry upload:
+//
+//  * tris   leaf-ordered FlatTri records, 48 B: (v0.xyz, e1.x), (e1.yz, e2.xy), (e2.z, face, 0, 0)
+//           -- record i is faces[face_indices[i]] with the edges glm::intersectRayTriangle forms
+//           (v1 - v0, v2 - v0 in fp32, gtx/intersect.inl:37-38), so a leaf's triangles are one
+//           contiguous, 16-B aligned run instead of three dependent gathers per triangle;
+//  * depth  the deepest leaf (sizes the traversal stack), whether every node bound lies in the
+//           range where the filtered slab test is proven (rt_fast.h), and the largest leaf.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "rt_abi.h"
+
+struct MirrorHost {
+    std::vector<float> tris;      // 12 floats per record
+    int depth = 0;                // deepest leaf (root = 0) reachable from node 0
+    bool fast = true;             // node bounds inside the filtered-slab range (rt_fast.h)
+    uint32_t hot_first = 0, hot_count = 0;  // largest leaf, if 9..512 triangles
+};
+
+// Build from host copies of the reference arrays.  node_count / face_count / vertex_count
+// bound the indices (out-of-range references throw std::runtime_error).
+void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t* face_indices, size_t index_count,
+                     const GPUFace* faces, size_t face_count, const GPUVertex* vertices, size_t vertex_count,
+                     MirrorHost* out);
+
+// Registry: device copies of a mirror, keyed by the GPUScene's BVH node pointer and valid
+// while the scene's face_indices / faces / vertices pointers are the ones it was built from.
+struct MirrorDevice {
+    const void* tris = nullptr;
+    int depth = -1;
+    bool fast = false;
+    uint32_t hot_first = 0, hot_count = 0;
+    bool owned = true;         // built by rt_scene_upload, which forgets it before freeing the arrays
+    uint64_t fingerprint = 0;  // foreign scenes: content hash of the arrays it was built from
+};
+// owned = false: a GPUScene filled by another host (the reference's Scene.cpp); the mirror is
+// then revalidated against `fingerprint` at every use (rt_kernel.hip foreign_mirror).
+int rt_internal_install_mirror(const GPUScene* scene, const MirrorHost& m, bool owned = true,
+                               uint64_t fingerprint = 0);  // 0 or -1 (rt_last_error)
+void rt_internal_forget_mirror(const void* gpu_nodes);
+bool rt_internal_lookup_mirror(const GPUScene* scene, MirrorDevice* out);
+
+void rt_internal_set_error(const char* msg);  // rt_last_error() text (rt_kernel.hip)

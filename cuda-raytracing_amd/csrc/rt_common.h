@@ -44,7 +44,8 @@ struct RenderArgs {
     unsigned long long* seg_counter;
     int scene_fast;  // all node bounds inside the filtered-slab range (rt_fast.h)
     uint32_t hot_first, hot_count;  // the scene's largest leaf (kept in LDS by each workgroup)
-    uint32_t tune;  // A/B knobs (RT_TUNE): bit0 no cooperative leaf rounds
+    uint32_t tune;  // A/B knobs (RT_TUNE, rt_render): bit0 no cooperative leaf rounds, bit1 no LDS hot
+                    // leaf, bit2 256-thread tiles, bit3 two-word stack entries
 };
 
 struct Counters {

@@ -374,7 +374,8 @@ __device__ __forceinline__ void coop_leaf(const float4* tris, const HotLeaf& hot
 // BVHRayHit for one lane (`live` = the lane has a segment to trace).  Every lane of the wave
 // must call it (it synchronises big leaves across the wave).  STRIDE: the stack's lane stride.
 template <int STRIDE, int SW, bool STATS, class C>
-__device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, const HotLeaf& hot, bool coop, uint32_t* stk,
+__device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, const HotLeaf& hot, uint32_t tune,
+                                      uint32_t* stk,
                                       const Ray& R, Hit& h, bool live, C& c) {
     bool active = false;
     uint32_t first = 0, count = 0;
@@ -422,8 +423,8 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
         if (__ballot(active && first == f0) == big) {
             const uint32_t k = (uint32_t)__popcll(big);
             const uint32_t chunks = (c0 + 63u) / 64u;
-            // cost model (VALU instructions): cooperative ~ k * (60 * chunks + 50), lane-parallel ~ 50 * c0
-            if (!STATS && coop && k * (60u * chunks + 50u) < 50u * c0) {
+            if (!STATS && (tune & 1u) == 0 && k * (60u * chunks + 50u) < 50u * c0) {
+                // cost model (VALU instructions): cooperative ~ k * (60 * chunks + 50), lane-parallel ~ 50 * c0
                 coop_leaf(tris, hot, big, f0, c0, R, h, c);
             } else if (hot.count != 0 && f0 == hot.first && c0 == hot.count) {
                 for (uint32_t i = 0; i < c0; i++) {

@@ -16,6 +16,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -28,8 +29,7 @@
 #include "rt_common.h"
 #include "rt_fast.h"
 
-bool rt_internal_lookup_mirror(const GPUScene* scene, const void** tris, int* depth, bool* scene_fast,
-                               uint32_t* hot_first, uint32_t* hot_count);
+#include "mirror.h"
 
 // ---------------------------------------------------------------------------------------
 // error state
@@ -46,6 +46,7 @@ static int check(hipError_t e, const char* what) {
 }
 
 extern "C" const char* rt_last_error(void) { return g_last_error.c_str(); }
+void rt_internal_set_error(const char* msg) { set_error(msg); }
 
 // ---------------------------------------------------------------------------------------
 // memory shim (utils/CUDAHelper.h:114-156)
@@ -541,7 +542,7 @@ __global__ __launch_bounds__(WG) void render_fast_kernel(RenderArgs a) {
             }
         }
         const rtfast::Ray R = rtfast::make_ray(ro, rd, nd, scene_fast);
-        rtfast::trace<WG, SW, STATS>(nodes4, tris, hot, (a.tune & 1u) == 0, stk, R, h, path, c);
+        rtfast::trace<WG, SW, STATS>(nodes4, tris, hot, a.tune, stk, R, h, path, c);
         if (!path) continue;
 
         bool end = false;
@@ -784,6 +785,90 @@ extern "C" int64_t rt_shard_tiles(int width, int height, int shard_index, int sh
     return tiles_of_shard(width, height, shard_index, shard_count);
 }
 
+// ---------------------------------------------------------------------------------------
+// Foreign scenes.  A GPUScene filled by another host (the reference's own Scene::Upload,
+// Scene.cpp:182-234) never registers a mirror.  On first use the arrays are read back, the
+// mirror is built exactly as rt_scene_upload builds it, and it is kept with a content
+// fingerprint of the four arrays; every later call re-hashes them on the GPU (~15 MB, a few
+// microseconds plus one 8-byte read-back) and rebuilds when they changed -- Scene::Upload
+// replaces buffers whose addresses the allocator may hand out again.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    x ^= x >> 31;
+    return x;
+}
+
+struct HashArrays {
+    const uint32_t* w[4];
+    unsigned long long n[4];  // words
+};
+
+__global__ __launch_bounds__(BLOCK) void fingerprint_kernel(HashArrays h, unsigned long long* out) {
+    unsigned long long acc = 0;
+    const unsigned long long stride = (unsigned long long)gridDim.x * BLOCK;
+    for (int k = 0; k < 4; k++) {
+        for (unsigned long long i = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x; i < h.n[k]; i += stride)
+            acc += mix64(((unsigned long long)k << 60) ^ (i << 32) ^ h.w[k][i]);
+    }
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);
+}
+
+static size_t bytes_from(const void* p) {
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (!p || hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) != hipSuccess) return 0;
+    return size - (size_t)((const char*)p - (const char*)base);
+}
+
+static int foreign_mirror(const GPUScene* scene, hipStream_t st, MirrorDevice* out) {
+    const size_t nb = bytes_from(scene->gpu_bvh_nodes), ni = bytes_from(scene->gpu_bvh_face_indices),
+                 nf = bytes_from(scene->gpu_faces), nv = bytes_from(scene->gpu_vertices);
+    if (!nb || !ni || !nf || !nv) return set_error("rt_render: scene arrays are not device allocations");
+    static unsigned long long* d_hash = nullptr;
+    static unsigned long long* h_hash = nullptr;
+    if (!d_hash && (hipMalloc(&d_hash, 8) != hipSuccess || hipHostMalloc(&h_hash, 8) != hipSuccess))
+        return set_error("rt_render: fingerprint buffers");
+    HashArrays h;
+    h.w[0] = (const uint32_t*)scene->gpu_bvh_nodes, h.n[0] = nb / 4;
+    h.w[1] = scene->gpu_bvh_face_indices, h.n[1] = ni / 4;
+    h.w[2] = (const uint32_t*)scene->gpu_faces, h.n[2] = nf / 4;
+    h.w[3] = (const uint32_t*)scene->gpu_vertices, h.n[3] = nv / 4;
+    if (hipMemsetAsync(d_hash, 0, 8, st) != hipSuccess) return set_error("rt_render: fingerprint");
+    hipLaunchKernelGGL(fingerprint_kernel, dim3(1024), dim3(BLOCK), 0, st, h, d_hash);
+    if (hipMemcpyAsync(h_hash, d_hash, 8, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+        return set_error("rt_render: fingerprint");
+    const unsigned long long fp = *h_hash ^ ((unsigned long long)nb << 1) ^ ((unsigned long long)nv << 33);
+    MirrorDevice m;
+    if (rt_internal_lookup_mirror(scene, &m) && !m.owned && m.fingerprint == fp) {
+        *out = m;
+        return 0;
+    }
+    std::vector<GPUBVHNode> nodes(nb / sizeof(GPUBVHNode));
+    std::vector<uint32_t> fi(ni / 4);
+    std::vector<GPUFace> faces(nf / sizeof(GPUFace));
+    std::vector<GPUVertex> verts(nv / sizeof(GPUVertex));
+    if (hipMemcpy(nodes.data(), scene->gpu_bvh_nodes, nodes.size() * sizeof(GPUBVHNode), hipMemcpyDeviceToHost) ||
+        hipMemcpy(fi.data(), scene->gpu_bvh_face_indices, fi.size() * 4, hipMemcpyDeviceToHost) ||
+        hipMemcpy(faces.data(), scene->gpu_faces, faces.size() * sizeof(GPUFace), hipMemcpyDeviceToHost) ||
+        hipMemcpy(verts.data(), scene->gpu_vertices, verts.size() * sizeof(GPUVertex), hipMemcpyDeviceToHost))
+        return set_error("rt_render: reading back the scene arrays failed");
+    MirrorHost mh;
+    try {
+        rt_build_mirror(nodes.data(), nodes.size(), fi.data(), fi.size(), faces.data(), faces.size(), verts.data(),
+                        verts.size(), &mh);
+    } catch (const std::exception& e) {
+        return set_error(std::string("rt_render: ") + e.what());
+    }
+    if (rt_internal_install_mirror(scene, mh, false, fp) != 0) return 1;
+    if (!rt_internal_lookup_mirror(scene, out)) return set_error("rt_render: mirror registry");
+    return 0;
+}
+
 extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void* stream) {
     if (!p || !scene) return set_error("rt_render: null argument");
     if (p->width <= 0 || p->height <= 0 || p->spp <= 0 || p->bounces < 0)
@@ -828,22 +913,26 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
 
     const int tiles = tiles_of_shard(p->width, p->height, p->shard_index, p->shard_count);
     if (tiles == 0) return 0;
-    const void* tris = nullptr;
-    int depth = -1;
-    bool scene_fast = false;
-    uint32_t hot_first = 0, hot_count = 0;
-    rt_internal_lookup_mirror(scene, &tris, &depth, &scene_fast, &hot_first, &hot_count);
-    static const char* tune = std::getenv("RT_TUNE");  // A/B knobs: bit0 no coop rounds, bit1 no LDS hot leaf, bit2 256-thread tiles, bit3 two-word stack entries
+    const bool want_ref = (p->flags & RT_RENDER_TRACER_REF) != 0;
+    MirrorDevice mir;
+    if ((!rt_internal_lookup_mirror(scene, &mir) || !mir.owned) && !want_ref) {
+        // not uploaded through rt_scene_upload: build / revalidate a private mirror
+        if (foreign_mirror(scene, (hipStream_t)stream, &mir) != 0) return 1;
+    }
+    const void* tris = mir.tris;
+    const int depth = mir.depth;
+    const bool scene_fast = mir.fast;
+    static const char* tune = std::getenv("RT_TUNE");  // A/B knobs (RenderArgs::tune)
     a.tune = tune ? (uint32_t)std::strtoul(tune, nullptr, 0) : 0u;
-    a.hot_first = hot_first;
-    a.hot_count = (a.tune & 2u) ? 0u : hot_count;
+    a.hot_first = mir.hot_first;
+    a.hot_count = (a.tune & 2u) ? 0u : mir.hot_count;
     static const bool force_ref = std::getenv("RT_FORCE_REFERENCE_LAYOUT") != nullptr;  // A/B switch
     a.tris = force_ref ? nullptr : (const FlatTri*)tris;
     const bool stats = (p->flags & RT_RENDER_STATS) != 0;
     hipStream_t s = (hipStream_t)stream;
     static const char* which = std::getenv("RT_TRACER");  // A/B switch: ref | flat | fast (default)
     const bool want_flat = (p->flags & RT_RENDER_TRACER_FLAT) || (which && std::strcmp(which, "flat") == 0);
-    if ((p->flags & RT_RENDER_TRACER_REF) || (which && std::strcmp(which, "ref") == 0)) a.tris = nullptr;
+    if (want_ref || (which && std::strcmp(which, "ref") == 0)) a.tris = nullptr;
     a.scene_fast = scene_fast ? 1 : 0;
     hipError_t e;
     if (!a.tris)
@@ -917,3 +1006,4 @@ extern "C" void init_rng(uint32_t thread_block_count, uint32_t thread_block_size
                        (rt_rng_state*)states, jump, seed, count, 0, 0, 0, 0, 0);
     if (check(hipGetLastError(), "init_rng_kernel launch")) std::printf("(init_rng) failed: %s\n", rt_last_error());
 }
+

@@ -2,6 +2,7 @@
 // RayTracing/BVH.cpp and the scene setup of RayTracing/RayTracing.cpp (file:line cited per
 // function) so that the arrays handed to the kernel are byte-identical to the reference's.
 #include "scene.h"
+#include "mirror.h"
 
 #include <algorithm>
 #include <cmath>
@@ -9,54 +10,6 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
-#include <map>
-#include <mutex>
-
-namespace {
-struct Mirror {
-    const void* face_indices;
-    const void* vertices;
-    const void* faces;
-    const void* tris;
-    int depth;
-    bool fast;
-    uint32_t hot_first, hot_count;
-};
-std::mutex g_mirror_mutex;
-std::map<const void*, Mirror> g_mirrors;  // keyed by the device BVH node array
-}  // namespace
-
-void rt_internal_register_mirror(const GPUScene* s, const void* tris, int depth, bool fast, uint32_t hot_first,
-                                 uint32_t hot_count) {
-    std::lock_guard<std::mutex> lock(g_mirror_mutex);
-    g_mirrors[s->gpu_bvh_nodes] =
-        Mirror{s->gpu_bvh_face_indices, s->gpu_vertices, s->gpu_faces, tris, depth, fast, hot_first, hot_count};
-}
-void rt_internal_forget_mirror(const void* gpu_nodes) {
-    std::lock_guard<std::mutex> lock(g_mirror_mutex);
-    g_mirrors.erase(gpu_nodes);
-}
-// The leaf-ordered triangle mirror is used only while ALL the reference arrays it was built
-// from are still the ones the GPUScene points at.
-bool rt_internal_lookup_mirror(const GPUScene* s, const void** tris, int* depth, bool* fast, uint32_t* hot_first,
-                               uint32_t* hot_count) {
-    std::lock_guard<std::mutex> lock(g_mirror_mutex);
-    auto it = g_mirrors.find(s->gpu_bvh_nodes);
-    *tris = nullptr;
-    *depth = -1;
-    *fast = false;
-    *hot_first = *hot_count = 0;
-    if (it == g_mirrors.end()) return false;
-    const Mirror& m = it->second;
-    *depth = m.depth;
-    *fast = m.fast;
-    *hot_first = m.hot_first;
-    *hot_count = m.hot_count;
-    if (m.face_indices != s->gpu_bvh_face_indices || m.vertices != s->gpu_vertices || m.faces != s->gpu_faces)
-        return false;
-    *tris = m.tris;
-    return true;
-}
 
 namespace RayTracing {
 
@@ -387,42 +340,12 @@ void Scene::Upload(void* rng) {
         upload(*faces_memory, faces.data(), nf);
     }
     if (tris_pending) {
-        // Leaf-ordered triangle mirror (kernel FlatTri): for BVH slot i, face f =
-        // face_indices[i]: (v0.xyz, e1.x), (e1.yz, e2.xy), (e2.z, f, 0, 0) with e1 = v1 - v0,
-        // e2 = v2 - v0 as glm::intersectRayTriangle forms them (gtx/intersect.inl:37-38).
+        // the kernel's private triangle mirror (mirror.h), built from the arrays just uploaded
+        MirrorHost m;
         const std::vector<uint32_t>& fi = bvh->GetFaceIndices();
-        std::vector<float> t(fi.size() * 12, 0.0f);
-        for (size_t i = 0; i < fi.size(); i++) {
-            const GPUFace& f = faces[fi[i]];
-            const float* p0 = vertices[f.v0].position;
-            const float* p1 = vertices[f.v1].position;
-            const float* p2 = vertices[f.v2].position;
-            float* o = &t[i * 12];
-            o[0] = p0[0], o[1] = p0[1], o[2] = p0[2];
-            o[3] = p1[0] - p0[0], o[4] = p1[1] - p0[1], o[5] = p1[2] - p0[2];
-            o[6] = p2[0] - p0[0], o[7] = p2[1] - p0[1], o[8] = p2[2] - p0[2];
-            uint32_t id = fi[i];
-            std::memcpy(&o[9], &id, 4);
-        }
-        tris_memory = std::make_unique<DeviceMemory>(t.size() * sizeof(float));
-        upload(*tris_memory, t.data(), t.size() * sizeof(float));
-        // rt_fast.h filtered slab tests need every node bound component to be 0 or have a
-        // magnitude in [2^-60, 2^62]; otherwise the kernel uses exact quotients throughout.
-        bool fast = true;
-        const GPUBVHNode* bn = bvh->GetGPUBVHNodes();
-        for (size_t n = 0; n < bvh->GetNodeCount() && fast; n++)
-            for (int k = 0; k < 3; k++) {
-                const float lo = std::fabs(bn[n].bmin[k]), hi = std::fabs(bn[n].bmax[k]);
-                if ((lo != 0.0f && (lo < 0x1p-60f || lo > 0x1p62f)) || (hi != 0.0f && (hi < 0x1p-60f || hi > 0x1p62f)))
-                    fast = false;
-            }
-        // The largest leaf stays resident in each workgroup's LDS (kernel rtfast::HotLeaf) when it
-        // is big enough to matter and small enough to fit (the bunny scene's floor leaf: 345).
-        uint32_t hot_first = 0, hot_count = 0;
-        for (size_t n = 0; n < bvh->GetNodeCount(); n++)
-            if (bn[n].prim_count > hot_count) hot_count = bn[n].prim_count, hot_first = bn[n].first_index;
-        if (hot_count <= 8 || hot_count > 512) hot_first = hot_count = 0;
-        rt_internal_register_mirror(this, tris_memory->GetMemory(), bvh->GetMaxDepth(), fast, hot_first, hot_count);
+        rt_build_mirror(bvh->GetGPUBVHNodes(), bvh->GetNodeCount(), fi.data(), fi.size(), faces.data(), faces.size(),
+                        vertices.data(), vertices.size(), &m);
+        if (rt_internal_install_mirror(this, m) != 0) throw std::runtime_error(rt_last_error());
         tris_pending = false;
     }
     dirty_flags = 0;
@@ -689,6 +612,32 @@ int rt_scene_upload(rt_scene* s, void* rng_state) {
     return 0;
 }
 const GPUScene* rt_scene_gpu(const rt_scene* s) { return &s->scene; }
+
+static int host_mirror(rt_scene* s, MirrorHost* m) {
+    try {
+        s->scene.BuildHost();
+        const auto& bvh = s->scene.GetBVH();
+        const auto& fi = bvh.GetFaceIndices();
+        rt_build_mirror(bvh.GetGPUBVHNodes(), bvh.GetNodeCount(), fi.data(), fi.size(), s->scene.HostFaces().data(),
+                        s->scene.HostFaces().size(), s->scene.HostVertices().data(), s->scene.HostVertices().size(), m);
+    } catch (const std::exception& e) {
+        rt_internal_set_error(e.what());
+        return -1;
+    }
+    return 0;
+}
+int rt_scene_mirror_info(rt_scene* s, size_t* tri_records) {
+    MirrorHost m;
+    if (host_mirror(s, &m) != 0) return -1;
+    *tri_records = m.tris.size() / 12;
+    return 0;
+}
+int rt_scene_mirror_copy(rt_scene* s, float* tris) {
+    MirrorHost m;
+    if (host_mirror(s, &m) != 0) return -1;
+    std::copy(m.tris.begin(), m.tris.end(), tris);
+    return 0;
+}
 void rt_scene_build(rt_scene* s) { s->scene.BuildHost(); }
 void rt_scene_camera(const rt_scene* s, GPUCamera* out) {
     *out = static_cast<const GPUCamera&>(const_cast<Scene&>(s->scene).GetCamera());

@@ -131,7 +131,7 @@ struct Scene : public GPUScene {
     std::vector<GPUFace> faces;
     std::vector<GPUVertex> vertices;
     std::unique_ptr<DeviceMemory> memory, materials_memory, bvh_memory, bvh_face_index_memory, faces_memory,
-        vertices_memory, tris_memory;
+        vertices_memory;
     uint64_t environment = 0;
     std::vector<float> environment_texels;
     int environment_size = 0;
@@ -151,10 +151,4 @@ void SetupPlaneGrid(Scene& scene, int n);
 
 }  // namespace RayTracing
 
-// Leaf-ordered triangle mirror + BVH depth registered by Scene::Upload for the device
-// arrays of a GPUScene (kernel fast path and stack sizing; see rt_kernel.hip).
-void rt_internal_register_mirror(const GPUScene* scene, const void* tris, int depth, bool fast, uint32_t hot_first,
-                                 uint32_t hot_count);
-void rt_internal_forget_mirror(const void* gpu_nodes);
-bool rt_internal_lookup_mirror(const GPUScene* scene, const void** tris, int* depth, bool* fast, uint32_t* hot_first,
-                               uint32_t* hot_count);
+#include "mirror.h"  // rt_internal_* mirror registry

@@ -267,6 +267,12 @@ size_t rt_scene_host_arrays(const rt_scene* scene, const GPUBVHNode** nodes, siz
                             size_t* vertex_count, const GPUFace** faces);
 int rt_scene_bvh_max_depth(const rt_scene* scene);
 
+/* Diagnostics for the tests: the kernel's private leaf-ordered triangle mirror
+   (cuda-raytracing_amd/csrc/mirror.h, 12 floats per record) built on the host from the scene's
+   host arrays.  Returns 0, or -1 with rt_last_error(). */
+int rt_scene_mirror_info(rt_scene* scene, size_t* tri_records);
+int rt_scene_mirror_copy(rt_scene* scene, float* tris);
+
 /* XORWOW jump matrix A^(4^k * 2^67) (k < 32) as 800 uint32 words in rocrand's layout
  * m[i*160 + j*5 + w] (input word i, bit j, output word w).  For tests. */
 int rt_xorwow_jump_matrix(int k, uint32_t out[800]);

@@ -21,7 +21,8 @@ def load_rt():
     if "cuda_raytracing_amd" in sys.modules:
         return sys.modules["cuda_raytracing_amd"]
     spec = importlib.util.spec_from_file_location(
-        "cuda_raytracing_amd", os.path.join(ROOT, "cuda-raytracing_amd", "__init__.py"))
+        "cuda_raytracing_amd", os.path.join(ROOT, "cuda-raytracing_amd", "__init__.py"),
+        submodule_search_locations=[os.path.join(ROOT, "cuda-raytracing_amd")])
     mod = importlib.util.module_from_spec(spec)
     sys.modules["cuda_raytracing_amd"] = mod
     spec.loader.exec_module(mod)

@@ -1,0 +1,88 @@
+"""World-size-2 (and 3) CPU rehearsal of the multi-GPU path with the gloo backend.
+
+The GPU box runs the same code with RCCL: bench.py renders each rank's tiles into a compact
+shard (rt_render shard mode), gathers the shards to rank 0 with sharding.gather_shards, and
+unshards them there.  Here the shards are cut from a frame the oracle rendered (the kernels
+need a GPU; tests/test_gpu_parity.py checks rt_render's shards and rt_unshard bit for bit),
+so this covers the tile deal, the compact-shard slot order, the collective and the
+reassembly.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import rt_testlib as T
+
+W, H = 72, 40  # ragged: neither side is a multiple of the 16-pixel tile
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, frame, result_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rt = T.load_rt()
+        sh = rt.sharding
+        per_shard = max(sh.tiles_of_shard(W, H, r, world) for r in range(world))
+        assert rt.shard_tiles(W, H, rank, world) == sh.tiles_of_shard(W, H, rank, world)
+        xs, ys = sh.slot_pixels(W, H, rank, world, per_shard)
+        shard = np.zeros((per_shard * sh.TILE_PIXELS, 4), dtype=np.float32)
+        ok = xs >= 0
+        shard[ok] = frame[ys[ok], xs[ok]]
+        got = sh.gather_shards(torch.from_numpy(shard), rank, world)
+        if rank == 0:
+            img, seen = sh.unshard_host(got.numpy(), W, H)
+            result_q.put((img, seen))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_reassembles_frame(world):
+    osc = T.OracleScene("bunny")
+    frame = osc.render(W, H, 1, 2, rng=T.oracle_rng_frame(0xDEADBEEF, W, H, 4), threads=4)
+    frame = np.ascontiguousarray(frame.reshape(H, W, 4), dtype=np.float32)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, frame, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    img, seen = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert (seen == 1).all(), "every pixel is owned by exactly one rank"
+    assert np.array_equal(img, frame)
+
+
+def test_tile_deal_balanced_and_complete():
+    from itertools import chain
+    rt = T.load_rt()
+    sh = rt.sharding
+    for (w, h) in [(1920, 1080), (256, 256), (17, 1), (3840, 2160)]:
+        total = sh.tiles_total(w, h)
+        for n in (1, 2, 3, 8):
+            counts = [rt.shard_tiles(w, h, r, n) for r in range(n)]
+            assert sum(counts) == total
+            assert max(counts) - min(counts) <= 1
+            assert counts == [sh.tiles_of_shard(w, h, r, n) for r in range(n)]
+    # slot -> pixel map is a bijection onto the frame
+    n = 3
+    per = max(sh.tiles_of_shard(40, 24, r, n) for r in range(n))
+    pix = list(chain.from_iterable(zip(*[a[a >= 0] for a in sh.slot_pixels(40, 24, r, n, per)]) for r in range(n)))
+    assert len(pix) == 40 * 24 == len(set(pix))

@@ -193,3 +193,62 @@ def test_full_size_config2_properties(rt):
     for r0 in (0, 517, 1064):
         want = o.render(w, h, spp, bounces, rows=(r0, r0 + 16))
         assert_close(g1[r0:r0 + 16], want, f"config 2 rows {r0}..{r0 + 16}")
+
+
+def _dev_copy(rt, src_ptr, nbytes):
+    """A fresh hipMalloc'd copy (as the reference's CUDA::DeviceMemory would hold)."""
+    import ctypes
+    p = ctypes.c_void_p()
+    assert rt.lib().rt_malloc(ctypes.byref(p), nbytes) == 0
+    assert rt.lib().rt_memcpy_d2d(p, ctypes.c_void_p(src_ptr), nbytes) == 0
+    return p
+
+
+def test_foreign_gpuscene(rt):
+    """A GPUScene filled by another host (the reference's own Scene::Upload) -- no mirror was
+    registered for it: the fast path builds one on first use, equals the registered path, and
+    notices when the arrays change in place (revalidated by content fingerprint)."""
+    import ctypes
+    w, h = 64, 36
+    s = make_scene(rt, "bunny", w, h)
+    rng = rt.alloc_rng(w * h)
+    rt.init_rng_states(rng, w, h, T.SEED)
+    s.upload(rng.data_ptr())
+    rng0 = rng.clone()
+    ha = s.host_arrays()
+    g = s.gpu.contents
+    sizes = {"gpu_bvh_nodes": ha["nodes"].nbytes, "gpu_bvh_face_indices": ha["face_indices"].nbytes,
+             "gpu_vertices": ha["vertices"].nbytes, "gpu_faces": ha["faces"].nbytes,
+             "gpu_spheres": 32 * g.sphere_count, "gpu_materials": 64 * g.material_count}
+    f = rt.GPUScene()
+    ctypes.pointer(f)[0] = g
+    owned = {}
+    for k, n in sizes.items():
+        owned[k] = _dev_copy(rt, getattr(g, k), n)
+        setattr(f, k, owned[k].value)
+    frng = rng.clone()
+    f.rng_state = frng.data_ptr()
+    try:
+        def frame(scene, rng_buf, tracer="fast"):
+            rng_buf.copy_(rng0)
+            a, b = rt.alloc_surface(w, h), rt.alloc_surface(w, h)
+            rt.render(scene, a, b, w, h, 2, 6, tracer=tracer)
+            torch.cuda.synchronize()
+            return rt.surface_view(a, w).cpu().numpy().copy()
+
+        ref = frame(s, rng)
+        assert np.array_equal(frame(f, frng), ref)
+        assert np.array_equal(frame(f, frng), ref)  # cached mirror, fingerprint unchanged
+        # move every vertex in place (same buffer, same size): the mirror must follow
+        vert = ha["vertices"].copy().view(np.float32).reshape(-1, 8)
+        vert[:, 0] += np.float32(0.75)
+        src = torch.from_numpy(vert.reshape(-1).copy()).cuda()
+        assert rt.lib().rt_memcpy_d2d(owned["gpu_vertices"], ctypes.c_void_p(src.data_ptr()), vert.nbytes) == 0
+        torch.cuda.synchronize()
+        moved_fast = frame(f, frng)
+        moved_ref = frame(f, frng, tracer="ref")
+        assert not np.array_equal(moved_fast, ref)
+        assert np.array_equal(moved_fast, moved_ref)
+    finally:
+        for p in owned.values():
+            rt.lib().rt_free(p)

@@ -77,3 +77,21 @@ def test_bvh_invariants():
     for c in (first[inner], first[inner] + 1):  # children inside the parent box
         assert (nodes[c, :3] >= nodes[inner, :3]).all() and (nodes[c, 3:6] <= nodes[inner, 3:6]).all()
     assert s.max_depth() == 25
+
+
+def test_triangle_mirror_records():
+    """The kernel's leaf-ordered mirror (mirror.h): record i = faces[face_indices[i]] with the
+    fp32 edges glm forms (v1 - v0, v2 - v0; GPUFace field order v0, v2, v1) and the face id."""
+    s = T.product_scene("bunny")
+    tris = s.mirror()
+    a = s.host_arrays()
+    fi = np.frombuffer(a["face_indices"].tobytes(), dtype=np.uint32)
+    faces = np.frombuffer(a["faces"].tobytes(), dtype=np.uint32).reshape(-1, 4)
+    pos = np.frombuffer(a["vertices"].tobytes(), dtype=np.float32).reshape(-1, 8)[:, 0:3]
+    f = faces[fi]
+    v0, v2, v1 = pos[f[:, 0]], pos[f[:, 1]], pos[f[:, 2]]
+    assert tris.shape == (len(fi), 12)
+    assert np.array_equal(tris[:, 0:3], v0)
+    assert np.array_equal(tris[:, 3:6], v1 - v0)
+    assert np.array_equal(tris[:, 6:9], v2 - v0)
+    assert np.array_equal(tris[:, 9].view(np.uint32), fi)

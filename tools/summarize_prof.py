@@ -29,12 +29,16 @@ def main():
     ap.add_argument("--tag", required=True)
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
-    ap.add_argument("--kernel", default="render_fast_kernel<28, false, 64>")
+    ap.add_argument("--kernel", default=None, help="default: the timed render kernel with the most time")
     a = ap.parse_args()
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
 
     stats = os.path.join(a.src, "prof_trace", "run_kernel_stats.csv")
+    if a.kernel is None and os.path.exists(stats):
+        rows = [r for r in csv.DictReader(open(stats)) if short(r["Name"]).startswith("render_fast_kernel<")
+                and ", false," in short(r["Name"])]
+        a.kernel = short(max(rows, key=lambda r: float(r["TotalDurationNs"]))["Name"]) if rows else None
     summary = {"config": a.config, "kernel": a.kernel}
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(out, f"{a.tag}_kernel_stats.csv"))
