@@ -33,10 +33,11 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
         put_flat(&out->tris[i * 12], verts[fc.v0].position, verts[fc.v1].position, verts[fc.v2].position, f);
     }
 
-    // walk the tree from the root: depth, filtered-slab range, largest leaf
+    // walk the tree from the root: depth, filtered-slab range, big leaves
+    out->pairs.clear();
     out->depth = 0;
     out->fast = true;
-    out->hot_first = out->hot_count = 0;
+    std::vector<uint32_t> big;
     if (node_count == 0) return;
     std::vector<std::pair<uint32_t, int>> st{{0u, 0}};
     size_t visited = 0;
@@ -54,13 +55,40 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
         if (nd.prim_count > 0) {
             if ((size_t)nd.first_index + nd.prim_count > index_count) bad("leaf range out of range");
             out->depth = std::max(out->depth, d);
-            if (nd.prim_count > out->hot_count) out->hot_count = nd.prim_count, out->hot_first = nd.first_index;
+            if (nd.prim_count > MIRROR_BIG_LEAF) big.push_back(n);
         } else {
             st.push_back({nd.first_index, d + 1});
             st.push_back({nd.first_index + 1, d + 1});
         }
     }
-    if (out->hot_count <= 8 || out->hot_count > 512) out->hot_first = out->hot_count = 0;
+    std::sort(big.begin(), big.end());
+    big.erase(std::unique(big.begin(), big.end()), big.end());
+    for (uint32_t n : big) {
+        const GPUBVHNode& nd = nodes[n];
+        float* lead = &out->tris[(size_t)nd.first_index * 12];
+        uint32_t po;
+        std::memcpy(&po, &lead[10], 4);
+        uint32_t pf;
+        std::memcpy(&pf, &lead[11], 4);
+        if (pf) continue;  // two nodes sharing one leaf range
+        po = (uint32_t)(out->pairs.size() / 20);
+        pf = 1;
+        std::memcpy(&lead[10], &po, 4);
+        std::memcpy(&lead[11], &pf, 4);
+        for (uint32_t j = 0; j < nd.prim_count; j += 2) {
+            const float* a = &out->tris[((size_t)nd.first_index + j) * 12];
+            static const float zero[12] = {};
+            const float* b = j + 1 < nd.prim_count ? &out->tris[((size_t)nd.first_index + j + 1) * 12] : zero;
+            float q[20];
+            for (int c = 0; c < 9; c++) q[2 * c] = a[c], q[2 * c + 1] = b[c];
+            uint32_t fa, fb = 0;
+            std::memcpy(&fa, &a[9], 4);
+            if (b != zero) std::memcpy(&fb, &b[9], 4);
+            std::memcpy(&q[18], &fa, 4);
+            std::memcpy(&q[19], &fb, 4);
+            out->pairs.insert(out->pairs.end(), q, q + 20);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -71,7 +99,7 @@ struct Entry {
     const void* face_indices;
     const void* vertices;
     const void* faces;
-    void* block;  // device copy of the tris records
+    void* block;  // device copy of the tris and pair records
     MirrorDevice dev;
 };
 std::mutex g_mutex;
@@ -84,20 +112,19 @@ void release(Entry& e) {
 }  // namespace
 
 int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owned, uint64_t fingerprint) {
-    const size_t nt = m.tris.size() * 4;
+    const size_t nt = m.tris.size() * 4, np = m.pairs.size() * 4;
     void* block = nullptr;
-    if (rt_malloc(&block, nt + 64) != 0) return -1;
+    if (rt_malloc(&block, nt + np + 64) != 0) return -1;
     char* b = static_cast<char*>(block);
-    if (nt && rt_memcpy_h2d(b, m.tris.data(), nt) != 0) {
+    if ((nt && rt_memcpy_h2d(b, m.tris.data(), nt) != 0) || (np && rt_memcpy_h2d(b + nt, m.pairs.data(), np) != 0)) {
         rt_free(block);
         return -1;
     }
     Entry e{s->gpu_bvh_face_indices, s->gpu_vertices, s->gpu_faces, block, {}};
     e.dev.tris = b;
+    e.dev.pairs = np ? b + nt : nullptr;
     e.dev.depth = m.depth;
     e.dev.fast = m.fast;
-    e.dev.hot_first = m.hot_first;
-    e.dev.hot_count = m.hot_count;
     e.dev.owned = owned;
     e.dev.fingerprint = fingerprint;
     std::lock_guard<std::mutex> lock(g_mutex);

@@ -3,12 +3,17 @@
 // The reference arrays (GPUBVHNode / face_indices / GPUFace / GPUVertex, GPUScene.h:25-74)
 // stay authoritative; from them the host derives once per geometry upload:
 //
-//  * tris   leaf-ordered FlatTri records, 48 B: (v0.xyz, e1.x), (e1.yz, e2.xy), (e2.z, face, 0, 0)
+//  * tris   leaf-ordered FlatTri records, 48 B: (v0.xyz, e1.x), (e1.yz, e2.xy), (e2.z, face, po, pf)
 //           -- record i is faces[face_indices[i]] with the edges glm::intersectRayTriangle forms
 //           (v1 - v0, v2 - v0 in fp32, gtx/intersect.inl:37-38), so a leaf's triangles are one
 //           contiguous, 16-B aligned run instead of three dependent gathers per triangle;
-//  * depth  the deepest leaf (sizes the traversal stack), whether every node bound lies in the
-//           range where the filtered slab test is proven (rt_fast.h), and the largest leaf.
+//  * pairs  for every leaf of more than BIG (= rtfast::BIG) triangles, the same triangles two by
+//           two with each component interleaved, 80 B per pair: (v0x_a, v0x_b, v0y_a, v0y_b),
+//           (v0z, e1x), (e1y, e1z), (e2x, e2y), (e2z_a, e2z_b, face_a, face_b) -- the operand
+//           layout of packed fp32 instructions; an odd leaf ends with an all-zero triangle.  The
+//           leaf's first tris record holds po = its first pair, pf = 1 (0 for other leaves);
+//  * depth  the deepest leaf (sizes the traversal stack) and whether every node bound lies in
+//           the range where the filtered slab test is proven (rt_fast.h).
 #pragma once
 
 #include <cstddef>
@@ -17,11 +22,13 @@
 
 #include "rt_abi.h"
 
+constexpr uint32_t MIRROR_BIG_LEAF = 8;  // leaves above this get pair records (== rtfast::BIG)
+
 struct MirrorHost {
     std::vector<float> tris;      // 12 floats per record
+    std::vector<float> pairs;     // 20 floats per pair
     int depth = 0;                // deepest leaf (root = 0) reachable from node 0
     bool fast = true;             // node bounds inside the filtered-slab range (rt_fast.h)
-    uint32_t hot_first = 0, hot_count = 0;  // largest leaf, if 9..512 triangles
 };
 
 // Build from host copies of the reference arrays.  node_count / face_count / vertex_count
@@ -34,9 +41,9 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
 // while the scene's face_indices / faces / vertices pointers are the ones it was built from.
 struct MirrorDevice {
     const void* tris = nullptr;
+    const void* pairs = nullptr;
     int depth = -1;
     bool fast = false;
-    uint32_t hot_first = 0, hot_count = 0;
     bool owned = true;         // built by rt_scene_upload, which forgets it before freeing the arrays
     uint64_t fingerprint = 0;  // foreign scenes: content hash of the arrays it was built from
 };

@@ -43,9 +43,9 @@ struct RenderArgs {
     unsigned long long* stats;
     unsigned long long* seg_counter;
     int scene_fast;  // all node bounds inside the filtered-slab range (rt_fast.h)
-    uint32_t hot_first, hot_count;  // the scene's largest leaf (kept in LDS by each workgroup)
-    uint32_t tune;  // A/B knobs (RT_TUNE, rt_render): bit0 no cooperative leaf rounds, bit1 no LDS hot
-                    // leaf, bit2 256-thread tiles, bit3 two-word stack entries
+    const float4* pairs;  // big leaves' triangles in packed pairs (mirror.h) or null
+    uint32_t tune;  // A/B knobs (RT_TUNE, rt_render): bit0 no cooperative leaf rounds, bit1 no pair
+                    // records, bits 4-5 big-leaf mode (rt_kernel.hip launch_fast_t)
 };
 
 struct Counters {

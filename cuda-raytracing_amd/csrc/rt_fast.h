@@ -25,7 +25,8 @@
 
 namespace rtfast {
 
-constexpr int BIG = 8;  // leaves above this size wait for the wave
+constexpr int BIG = 8;     // leaves above this size wait for the wave (and have pair records)
+constexpr int WAVE = 64;  // lane stride of the LDS stack
 
 using rtm::f3;
 
@@ -142,54 +143,30 @@ __device__ __forceinline__ float4 ldc(ConstF4 p, uint32_t i) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
-// Pop stack entries until one passes `tmin < closest` (the reference's pop-time test).
-// SW == 2: entry = {node index | (tmin is exact) << 31, tmin bits}.
-// SW == 1: entry = node index; tmin is recomputed from the node (the same slab arithmetic gives
-// the same value, so the decision is the reference's), halving the LDS per lane.
-template <int WAVE, int SW>
+// Pop stack entries until one passes `tmin < closest` (the reference's pop-time test).  An
+// entry is a node index (lane stride WAVE in LDS); tmin is recomputed from the node with the same
+// slab arithmetic, so the decision is the reference's, at one word of LDS per entry.
 __device__ __forceinline__ bool pop(const float4* nodes4, uint32_t* stk, int& sp, const Ray& R, float best,
                                     uint32_t& first, uint32_t& count) {
     while (sp > 0) {
         sp--;
-        const uint32_t w0 = stk[(sp * SW) * WAVE];
-        const uint32_t idx = w0 & 0x7fffffffu;
-        bool pass;
-        if (SW == 1) {
-            const float4 lo = nodes4[2 * idx], hi = nodes4[2 * idx + 1];
-            int cl = UNSURE;
-            float te, tx;
-            if (R.fast) {
-                slab_approx(R, lo, hi, &te, &tx);
-                cl = classify_lt(te, best);
-            }
-            if (cl == UNSURE) {
-                slab_exact(R, lo, hi, &te, &tx);
-                pass = te < best;
-            } else {
-                pass = cl == YES;
-            }
-            if (pass) {
-                first = __float_as_uint(hi.z), count = __float_as_uint(hi.w);
-                return true;
-            }
-            continue;
+        const uint32_t idx = stk[sp * WAVE];
+        const float4 lo = nodes4[2 * idx], hi = nodes4[2 * idx + 1];
+        int cl = UNSURE;
+        float te, tx;
+        if (R.fast) {
+            slab_approx(R, lo, hi, &te, &tx);
+            cl = classify_lt(te, best);
         }
-        const float t = __uint_as_float(stk[(sp * SW + 1) * WAVE]);
-        if (w0 >> 31) {
-            pass = t < best;
+        bool pass;
+        if (cl == UNSURE) {
+            slab_exact(R, lo, hi, &te, &tx);
+            pass = te < best;
         } else {
-            const int cl = classify_lt(t, best);
-            if (cl == UNSURE) {
-                float te, tx;
-                slab_exact(R, nodes4[2 * idx], nodes4[2 * idx + 1], &te, &tx);
-                pass = te < best;
-            } else {
-                pass = cl == YES;
-            }
+            pass = cl == YES;
         }
         if (pass) {
-            const float4 nh = nodes4[2 * idx + 1];
-            first = __float_as_uint(nh.z), count = __float_as_uint(nh.w);
+            first = __float_as_uint(hi.z), count = __float_as_uint(hi.w);
             return true;
         }
     }
@@ -199,7 +176,7 @@ __device__ __forceinline__ bool pop(const float4* nodes4, uint32_t* stk, int& sp
 // One inner-node step: both children (adjacent in the node array) tested, the right child
 // continued in registers, the left one continued or pushed, exactly as the reference's
 // push(first), push(first+1), pop order.  Returns false when the lane must pop.
-template <int WAVE, int SW, bool STATS, class C>
+template <bool STATS, class C>
 __device__ __forceinline__ bool inner_step(const float4* nodes4, uint32_t* stk, int& sp, const Ray& R, float best,
                                            uint32_t& first, uint32_t& count, C& c) {
     const float4 l0 = nodes4[2 * first], l1 = nodes4[2 * first + 1];
@@ -225,12 +202,7 @@ __device__ __forceinline__ bool inner_step(const float4* nodes4, uint32_t* stk, 
     }
     if (rlt == YES) {
         if (okl == YES) {
-            if (SW == 1) {
-                stk[sp * WAVE] = first;
-            } else {
-                stk[(sp * 2) * WAVE] = first | (exact_l ? 0x80000000u : 0u);
-                stk[(sp * 2 + 1) * WAVE] = __float_as_uint(tl);
-            }
+            stk[sp * WAVE] = first;
             sp++;
         }
         first = __float_as_uint(r1.z), count = __float_as_uint(r1.w);
@@ -258,13 +230,16 @@ __device__ __forceinline__ bool inner_step(const float4* nodes4, uint32_t* stk, 
     return false;
 }
 
-// A leaf kept resident in LDS by the workgroup (the scene's largest leaf; SoA records).
-struct HotLeaf {
-    const float4* a;  // LDS
-    const float4* b;
-    const float4* c;
-    uint32_t first, count;  // count 0: none
-};
+// glm's accept predicate from the four quantities (det, u, v, u + v), as test_triangle.
+__device__ __forceinline__ bool tri_ok(float det, float u, float v, float uv) {
+    const float eps = 1.1920928955078125e-07f;
+    const uint32_t sgn = __float_as_uint(det) & 0x80000000u;
+    const float adet = fabsf(det);
+    const float su = __uint_as_float(__float_as_uint(u) ^ sgn);
+    const float sv = __uint_as_float(__float_as_uint(v) ^ sgn);
+    const float suv = __uint_as_float(__float_as_uint(uv) ^ sgn);
+    return adet > eps && !(su < 0.0f || su > adet) && !(sv < 0.0f || suv > adet);
+}
 
 // glm::intersectRayTriangle + BVHRayHit's accept test (`!(t >= best || t < 0)`) for one
 // candidate; returns whether it would be accepted against threshold `best`, and reports a
@@ -272,7 +247,6 @@ struct HotLeaf {
 // a min-reduction would not, so such a ray is redone sequentially).
 __device__ __forceinline__ bool tri_accept(f3 o, f3 nd, float4 A, float4 B, float4 Cc, float best, float* t_o,
                                            float* bx, float* by, bool* nan) {
-    const float eps = 1.1920928955078125e-07f;
     const f3 e1 = rtm::mk(A.w, B.x, B.y), e2 = rtm::mk(B.z, B.w, Cc.x);
     const f3 p = rtm::cross(nd, e2);
     const float det = rtm::dot(e1, p);
@@ -281,13 +255,7 @@ __device__ __forceinline__ bool tri_accept(f3 o, f3 nd, float4 A, float4 B, floa
     const f3 perp = rtm::cross(dist, e1);
     const float v = rtm::dot(nd, perp);
     const float uv = u + v;
-    const uint32_t sgn = __float_as_uint(det) & 0x80000000u;
-    const float adet = fabsf(det);
-    const float su = __uint_as_float(__float_as_uint(u) ^ sgn);
-    const float sv = __uint_as_float(__float_as_uint(v) ^ sgn);
-    const float suv = __uint_as_float(__float_as_uint(uv) ^ sgn);
-    const bool ok = adet > eps && !(su < 0.0f || su > adet) && !(sv < 0.0f || suv > adet);
-    if (!ok) return false;
+    if (!tri_ok(det, u, v, uv)) return false;
     const float inv_det = 1.0f / det;
     const float t = rtm::dot(e2, perp) * inv_det;
     *nan = *nan || (t != t);
@@ -298,39 +266,123 @@ __device__ __forceinline__ bool tri_accept(f3 o, f3 nd, float4 A, float4 B, floa
     return true;
 }
 
+// ---------------------------------------------------------------------------------------
+// Big leaves in packed pairs.  For every leaf above BIG triangles the mirror also holds the
+// triangles two by two, each component interleaved (mirror.h), so one packed fp32 instruction
+// (v_pk_mul_f32 / v_pk_add_f32) does the same IEEE operation for two triangles -- per half
+// exactly the scalar result, so the decisions are the reference's.  An odd leaf is padded with
+// an all-zero triangle (det = 0 is never accepted).
+// ---------------------------------------------------------------------------------------
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+struct Pair {
+    f2 v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z;
+    uint32_t fa, fb;  // face ids
+};
+
+__device__ __forceinline__ Pair make_pair(f4v q0, f4v q1, f4v q2, f4v q3, f4v q4) {
+    Pair P;
+    P.v0x = q0.xy, P.v0y = q0.zw, P.v0z = q1.xy;
+    P.e1x = q1.zw, P.e1y = q2.xy, P.e1z = q2.zw;
+    P.e2x = q3.xy, P.e2y = q3.zw, P.e2z = q4.xy;
+    P.fa = __float_as_uint(q4.z), P.fb = __float_as_uint(q4.w);
+    return P;
+}
+__device__ __forceinline__ Pair ld_pair_scalar(ConstF4 base, uint32_t p) {
+    return make_pair(base[5 * p], base[5 * p + 1], base[5 * p + 2], base[5 * p + 3], base[5 * p + 4]);
+}
+__device__ __forceinline__ Pair ld_pair(const float4* base, uint32_t p) {
+    const f4v* q = reinterpret_cast<const f4v*>(base) + 5 * (size_t)p;
+    return make_pair(q[0], q[1], q[2], q[3], q[4]);
+}
+
+// det, u, v, u + v and perp of glm::intersectRayTriangle for both triangles (same operation
+// order as test_triangle: p = cross(nd, e2), det = dot(e1, p), dist = o - v0, u = dot(dist, p),
+// perp = cross(dist, e1), v = dot(nd, perp)).
+struct PairEval {
+    f2 det, u, v, uv, qx, qy, qz;  // q = perp
+};
+__device__ __forceinline__ PairEval pair_eval(f3 o, f3 nd, const Pair& P) {
+    const f2 ndx = nd.x, ndy = nd.y, ndz = nd.z;
+    const f2 px = ndy * P.e2z - P.e2y * ndz;
+    const f2 py = ndz * P.e2x - P.e2z * ndx;
+    const f2 pz = ndx * P.e2y - P.e2x * ndy;
+    PairEval E;
+    E.det = (P.e1x * px + P.e1y * py) + P.e1z * pz;
+    const f2 dx = o.x - P.v0x, dy = o.y - P.v0y, dz = o.z - P.v0z;
+    E.u = (dx * px + dy * py) + dz * pz;
+    E.qx = dy * P.e1z - P.e1y * dz;
+    E.qy = dz * P.e1x - P.e1z * dx;
+    E.qz = dx * P.e1y - P.e1x * dy;
+    E.v = (ndx * E.qx + ndy * E.qy) + ndz * E.qz;
+    E.uv = E.u + E.v;
+    return E;
+}
+
+// The distance of an accepted pair member (rare path, scalar).
+__device__ __forceinline__ float pair_t(const Pair& P, const PairEval& E, int k, float* inv) {
+    const float det = k ? E.det.y : E.det.x;
+    *inv = 1.0f / det;
+    const f3 e2 = k ? rtm::mk(P.e2x.y, P.e2y.y, P.e2z.y) : rtm::mk(P.e2x.x, P.e2y.x, P.e2z.x);
+    const f3 q = k ? rtm::mk(E.qx.y, E.qy.y, E.qz.y) : rtm::mk(E.qx.x, E.qy.x, E.qz.x);
+    return rtm::dot(e2, q) * *inv;
+}
+
+// BVHRayHit's sequential leaf step for triangles 2p, 2p+1 (in that order) on this lane's ray.
+__device__ __forceinline__ void pair_test(const Ray& R, const Pair& P, Hit& h) {
+    const PairEval E = pair_eval(R.o, R.nd, P);
+    const bool oka = tri_ok(E.det.x, E.u.x, E.v.x, E.uv.x);
+    const bool okb = tri_ok(E.det.y, E.u.y, E.v.y, E.uv.y);
+    if (oka) {
+        float inv;
+        const float t = pair_t(P, E, 0, &inv);
+        if (!(t >= h.best || t < 0.0f)) h.best = t, h.kind = 2, h.id = P.fa, h.bx = E.u.x * inv, h.by = E.v.x * inv;
+    }
+    if (okb) {
+        float inv;
+        const float t = pair_t(P, E, 1, &inv);
+        if (!(t >= h.best || t < 0.0f)) h.best = t, h.kind = 2, h.id = P.fb, h.bx = E.u.y * inv, h.by = E.v.y * inv;
+    }
+}
+
 __device__ __forceinline__ float bcast(float v, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
 
-// Cooperative big-leaf round: the waiting lanes (mask `big`) all wait at leaf [f0, f0+c0).
-// Rays are taken one at a time; the 64 lanes split the leaf's triangles (lane l tests
-// l, l+64, ...), each keeping its first strictly-closer candidate, and a (t, index)
-// lexicographic arg-min over the wave gives exactly the triangle the sequential loop
-// would end on (the first index attaining the minimum t below the ray's closest distance).
-template <class C>
-__device__ __forceinline__ void coop_leaf(const float4* tris, const HotLeaf& hot, unsigned long long big, uint32_t f0,
-                                          uint32_t c0, const Ray& R, Hit& h, C& c) {
+// Cooperative big-leaf round: the waiting lanes (mask `big`) all wait at leaf [f0, f0+c0),
+// whose pairs start at `pairs`.  Rays are taken one at a time; lane l tests pairs l, l+64, ...
+// keeping its first strictly-closer candidate, and a (t, index) lexicographic arg-min over the
+// wave gives exactly the triangle the sequential loop ends on (the first index attaining the
+// minimum t below the ray's closest distance).  A NaN distance sends the ray to the sequential
+// loop.
+__device__ __forceinline__ void coop_leaf(const float4* tris, const float4* pairs, unsigned long long big, uint32_t f0,
+                                          uint32_t c0, const Ray& R, Hit& h) {
     const uint32_t lane = threadIdx.x & 63u;
-    const bool resident = hot.count != 0 && f0 == hot.first && c0 == hot.count;
+    const uint32_t np = (c0 + 1u) / 2u;
     unsigned long long m = big;
     while (m) {
         const int r = __ffsll((long long)m) - 1;
         m &= m - 1;
         const f3 rox = rtm::mk(bcast(R.o.x, r), bcast(R.o.y, r), bcast(R.o.z, r));
         const f3 nd = rtm::mk(bcast(R.nd.x, r), bcast(R.nd.y, r), bcast(R.nd.z, r));
-        const float best0 = bcast(h.best, r);
-        float bt = best0, bx = 0.0f, by = 0.0f;
-        uint32_t bi = 0xffffffffu;
+        float bt = bcast(h.best, r), bx = 0.0f, by = 0.0f;
+        uint32_t bi = 0xffffffffu, bid = 0;
         bool nan = false;
-        for (uint32_t j = lane; j < c0; j += 64u) {
-            float4 A, B, Cc;
-            if (resident) {
-                A = hot.a[j], B = hot.b[j], Cc = hot.c[j];
-            } else {
-                A = tris[3 * (f0 + j)], B = tris[3 * (f0 + j) + 1], Cc = tris[3 * (f0 + j) + 2];
+        for (uint32_t p = lane; p < np; p += 64u) {
+            const Pair P = ld_pair(pairs, p);
+            const PairEval E = pair_eval(rox, nd, P);
+            if (tri_ok(E.det.x, E.u.x, E.v.x, E.uv.x)) {
+                float inv;
+                const float t = pair_t(P, E, 0, &inv);
+                nan = nan || (t != t);
+                if (!(t >= bt || t < 0.0f)) bt = t, bx = E.u.x * inv, by = E.v.x * inv, bi = 2 * p, bid = P.fa;
             }
-            float t, x, y;
-            if (tri_accept(rox, nd, A, B, Cc, bt, &t, &x, &y, &nan)) bt = t, bx = x, by = y, bi = j;
+            if (tri_ok(E.det.y, E.u.y, E.v.y, E.uv.y)) {
+                float inv;
+                const float t = pair_t(P, E, 1, &inv);
+                nan = nan || (t != t);
+                if (!(t >= bt || t < 0.0f)) bt = t, bx = E.u.y * inv, by = E.v.y * inv, bi = 2 * p + 1, bid = P.fb;
+            }
         }
         if (__ballot(nan)) {
             // sequential fallback for this ray (never taken for finite scenes)
@@ -359,95 +411,186 @@ __device__ __forceinline__ void coop_leaf(const float4* tris, const HotLeaf& hot
         }
         mi = __builtin_amdgcn_readfirstlane(mi);
         if (mi != 0xffffffffu) {
+            const int wl = (int)((mi >> 1) & 63u);  // lane that tested pair mi / 2
+            const float wbx = bcast(bx, wl), wby = bcast(by, wl), wt = bcast(bt, wl);
+            const uint32_t wid = (uint32_t)__builtin_amdgcn_readlane((int)bid, wl);
+            if ((int)lane == r) h.best = wt, h.kind = 2, h.bx = wbx, h.by = wby, h.id = wid;
+        }
+    }
+}
+
+// coop_leaf on the scalar records (lane l tests triangles l, l+64, ...).
+__device__ __forceinline__ void coop_leaf_scalar(const float4* tris, unsigned long long big, uint32_t f0, uint32_t c0,
+                                                 const Ray& R, Hit& h) {
+    const uint32_t lane = threadIdx.x & 63u;
+    unsigned long long m = big;
+    while (m) {
+        const int r = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const f3 rox = rtm::mk(bcast(R.o.x, r), bcast(R.o.y, r), bcast(R.o.z, r));
+        const f3 nd = rtm::mk(bcast(R.nd.x, r), bcast(R.nd.y, r), bcast(R.nd.z, r));
+        float bt = bcast(h.best, r), bx = 0.0f, by = 0.0f;
+        uint32_t bi = 0xffffffffu;
+        bool nan = false;
+        for (uint32_t j = lane; j < c0; j += 64u) {
+            const float4 A = tris[3 * (f0 + j)], B = tris[3 * (f0 + j) + 1], Cc = tris[3 * (f0 + j) + 2];
+            float t, x, y;
+            if (tri_accept(rox, nd, A, B, Cc, bt, &t, &x, &y, &nan)) bt = t, bx = x, by = y, bi = j;
+        }
+        if (__ballot(nan)) {
+            if ((int)lane == r) {
+                float t, x, y;
+                bool dummy = false;
+                for (uint32_t j = 0; j < c0; j++) {
+                    const float4 A = tris[3 * (f0 + j)], B = tris[3 * (f0 + j) + 1], Cc = tris[3 * (f0 + j) + 2];
+                    if (tri_accept(R.o, R.nd, A, B, Cc, h.best, &t, &x, &y, &dummy)) {
+                        h.best = t, h.kind = 2, h.bx = x, h.by = y;
+                        h.id = __float_as_uint(Cc.y);
+                    }
+                }
+            }
+            continue;
+        }
+        float mt = bt;
+        uint32_t mi = bi;
+        for (int off = 32; off > 0; off >>= 1) {
+            const float ot = __shfl_xor(mt, off);
+            const uint32_t oi = (uint32_t)__shfl_xor((int)mi, off);
+            const bool take = ot < mt || (ot == mt && oi < mi);
+            mt = take ? ot : mt;
+            mi = take ? oi : mi;
+        }
+        mi = __builtin_amdgcn_readfirstlane(mi);
+        if (mi != 0xffffffffu) {
             const int wl = (int)(mi & 63u);
             const float wbx = bcast(bx, wl), wby = bcast(by, wl), wt = bcast(bt, wl);
             if ((int)lane == r) {
-                const float4 Cc = resident ? hot.c[mi] : tris[3 * (f0 + mi) + 2];
+                const float4 Cc = tris[3 * (f0 + mi) + 2];
                 h.best = wt, h.kind = 2, h.bx = wbx, h.by = wby;
                 h.id = __float_as_uint(Cc.y);
             }
         }
     }
-    (void)c;
 }
 
 // BVHRayHit for one lane (`live` = the lane has a segment to trace).  Every lane of the wave
 // must call it (it synchronises big leaves across the wave).  STRIDE: the stack's lane stride.
-template <int STRIDE, int SW, bool STATS, class C>
-__device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, const HotLeaf& hot, uint32_t tune,
-                                      uint32_t* stk,
-                                      const Ray& R, Hit& h, bool live, C& c) {
-    bool active = false;
-    uint32_t first = 0, count = 0;
-    int sp = 0;
-    if (live) {
-        // root: IntersectAABB against the closest sphere distance
-        const float4 lo = nodes4[0], hi = nodes4[1];
-        if (STATS) c.node++;
-        float tmin, tmax;
-        slab_exact(R, lo, hi, &tmin, &tmax);
-        active = tmax >= tmin && tmin < h.best && tmax > 0.0f;
-        first = __float_as_uint(hi.z), count = __float_as_uint(hi.w);
+// Traversal state of one lane between steps: the node (or leaf) it is at and its stack depth.
+struct Trav {
+    uint32_t first, count;
+    int sp;
+};
+
+// IntersectAABB of the root against the closest sphere distance (main_raytracing.cu:37-45):
+// whether the lane has anything to traverse.
+template <bool STATS, class C>
+__device__ __forceinline__ bool trav_begin(const float4* nodes4, const Ray& R, const Hit& h, Trav& T, C& c) {
+    const float4 lo = nodes4[0], hi = nodes4[1];
+    if (STATS) c.node++;
+    float tmin, tmax;
+    slab_exact(R, lo, hi, &tmin, &tmax);
+    T.first = __float_as_uint(hi.z), T.count = __float_as_uint(hi.w), T.sp = 0;
+    return tmax >= tmin && tmin < h.best && tmax > 0.0f;
+}
+
+// One small step of a lane at a small leaf or an inner node; false when the traversal is over.
+template <bool STATS, class C>
+__device__ __forceinline__ bool small_step(const float4* nodes4, const float4* tris, uint32_t* stk, const Ray& R,
+                                           Hit& h, Trav& T, C& c) {
+    if (T.count > 0) {
+        for (uint32_t i = T.first; i < T.first + T.count; i++)
+            test_triangle<STATS>(R, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], h, c);
+        return pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
     }
+    if (inner_step<STATS>(nodes4, stk, T.sp, R, h.best, T.first, T.count, c)) return true;
+    return pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
+}
+
+// One big-leaf round, called by all lanes of the wave in converged control flow.  `big` = the
+// lanes waiting at a big leaf (`waiting` on this lane).  The lanes at the leaf of the lowest
+// waiting lane run it together (pairs / cooperative rounds / scalar loads); if every waiting
+// lane is at that leaf, or each lane alone otherwise (MODE: see trace).  Returns whether this
+// lane ran its leaf (it then pops; the others keep waiting).
+template <bool STATS, int MODE, class C>
+__device__ __forceinline__ bool big_round(const float4* tris, const float4* pairs, uint32_t tune, unsigned long long big,
+                                          bool waiting, const Ray& R, Hit& h, const Trav& T, C& c) {
+    const int l0 = __ffsll((long long)big) - 1;
+    const uint32_t f0 = __builtin_amdgcn_readlane(T.first, l0);
+    const uint32_t c0 = __builtin_amdgcn_readlane(T.count, l0);
+    if (STATS) {
+        uint32_t mx = waiting ? T.count : 0u;
+        for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
+        c.w_big += (threadIdx.x & 63) == 0 ? mx : 0;
+        c.l_big += waiting ? T.count : 0;
+    }
+    if (__ballot(waiting && T.first == f0) == big) {
+        // the first record of a big leaf says where its pairs are (mirror.h)
+        const f4v lead = ((ConstF4)(tris + 3 * (size_t)f0))[2];
+        const uint32_t k = (uint32_t)__popcll(big);
+        if (!STATS && MODE < 2 && pairs && __float_as_uint(lead.w) != 0u) {
+            const float4* lp = pairs + 5 * (size_t)__float_as_uint(lead.z);
+            const uint32_t np = (c0 + 1u) / 2u, chunks = (np + 63u) / 64u;
+            // cost model (VALU instructions per pair ~40): cooperative ~ k * (40 * chunks + 60),
+            // shared-leaf ~ 40 * np for all waiting lanes at once
+            const uint32_t cchunks = (c0 + 63u) / 64u;
+            if (MODE == 0 && (tune & 1u) == 0 && k * (40u * chunks + 60u) < 40u * np) {
+                coop_leaf(tris, lp, big, f0, c0, R, h);
+            } else if (MODE == 1 && (tune & 1u) == 0 && k * (60u * cchunks + 50u) < 40u * np) {
+                coop_leaf_scalar(tris, big, f0, c0, R, h);
+            } else {
+                ConstF4 ps = (ConstF4)lp;
+                for (uint32_t q = 0; q < np; q++, ps += 5) {
+                    const Pair P = ld_pair_scalar(ps, 0);
+                    if (waiting) pair_test(R, P, h);
+                }
+            }
+        } else if (!STATS && (tune & 1u) == 0 && k * (60u * ((c0 + 63u) / 64u) + 50u) < 50u * c0) {
+            // cost model (VALU instructions): cooperative ~ k * (60 * chunks + 50), lane-parallel ~ 50 * c0
+            coop_leaf_scalar(tris, big, f0, c0, R, h);
+        } else {
+            // all waiting lanes share one leaf: scalar loads, next record prefetched
+            ConstF4 st = (ConstF4)(tris + 3 * (size_t)f0);
+            ConstF4 const last = st + 3 * (c0 - 1);
+            float4 A = ldc(st, 0), B = ldc(st, 1), Cc = ldc(st, 2);
+            for (uint32_t i = 0; i < c0; i++) {
+                st = st == last ? st : st + 3;
+                const float4 An = ldc(st, 0), Bn = ldc(st, 1), Cn = ldc(st, 2);
+                if (waiting) test_triangle<STATS>(R, A, B, Cc, h, c);
+                A = An, B = Bn, Cc = Cn;
+            }
+        }
+        return waiting;
+    }
+    if (waiting) {
+        for (uint32_t i = T.first; i < T.first + T.count; i++)
+            test_triangle<STATS>(R, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], h, c);
+    }
+    return waiting;
+}
+
+// BVHRayHit for one lane (`live` = the lane has a segment to trace), every lane of the wave
+// calling.  Small steps run while any lane has one; big leaves wait until every lane is done
+// or waiting at one.  MODE 0: big leaves through pair records (shared-leaf loop and cooperative
+// rounds); 1: pairs in the shared-leaf loop, scalar cooperative rounds; 2: scalar records only.
+template <bool STATS, int MODE, class C>
+__device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, const float4* pairs, uint32_t tune,
+                                      uint32_t* stk, const Ray& R, Hit& h, bool live, C& c) {
+    Trav T{0, 0, 0};
+    bool active = live && trav_begin<STATS>(nodes4, R, h, T, c);
     for (;;) {
-        const bool small = active && count <= (uint32_t)BIG;
+        const bool small = active && T.count <= (uint32_t)BIG;
         if (__ballot(small)) {
             if (STATS) {
                 c.w_small += (threadIdx.x & 63) == 0;
                 c.l_small += small;
             }
-            if (small) {
-                if (count > 0) {
-                    for (uint32_t i = first; i < first + count; i++)
-                        test_triangle<STATS>(R, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], h, c);
-                    active = pop<STRIDE, SW>(nodes4, stk, sp, R, h.best, first, count);
-                } else if (!inner_step<STRIDE, SW, STATS>(nodes4, stk, sp, R, h.best, first, count, c)) {
-                    active = pop<STRIDE, SW>(nodes4, stk, sp, R, h.best, first, count);
-                }
-            }
+            if (small) active = small_step<STATS>(nodes4, tris, stk, R, h, T, c);
             continue;
         }
         const unsigned long long big = __ballot(active);
         if (!big) break;
-        // every waiting lane is at a big leaf: run them together
-        // the leaf of the lowest waiting lane (not lane 0: it may be done, with stale state)
-        const int l0 = __ffsll((long long)big) - 1;
-        const uint32_t f0 = __builtin_amdgcn_readlane(first, l0);
-        const uint32_t c0 = __builtin_amdgcn_readlane(count, l0);
-        if (STATS) {
-            uint32_t mx = active ? count : 0u;
-            for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
-            c.w_big += (threadIdx.x & 63) == 0 ? mx : 0;
-            c.l_big += active ? count : 0;
-        }
-        if (__ballot(active && first == f0) == big) {
-            const uint32_t k = (uint32_t)__popcll(big);
-            const uint32_t chunks = (c0 + 63u) / 64u;
-            if (!STATS && (tune & 1u) == 0 && k * (60u * chunks + 50u) < 50u * c0) {
-                // cost model (VALU instructions): cooperative ~ k * (60 * chunks + 50), lane-parallel ~ 50 * c0
-                coop_leaf(tris, hot, big, f0, c0, R, h, c);
-            } else if (hot.count != 0 && f0 == hot.first && c0 == hot.count) {
-                for (uint32_t i = 0; i < c0; i++) {
-                    const float4 A = hot.a[i], B = hot.b[i], Cc = hot.c[i];
-                    if (active) test_triangle<STATS>(R, A, B, Cc, h, c);
-                }
-            } else {
-                // all waiting lanes share one leaf: scalar loads, next record prefetched
-                ConstF4 st = (ConstF4)(tris + 3 * (size_t)f0);
-                ConstF4 const last = st + 3 * (c0 - 1);
-                float4 A = ldc(st, 0), B = ldc(st, 1), Cc = ldc(st, 2);
-                for (uint32_t i = 0; i < c0; i++) {
-                    st = st == last ? st : st + 3;
-                    const float4 An = ldc(st, 0), Bn = ldc(st, 1), Cn = ldc(st, 2);
-                    if (active) test_triangle<STATS>(R, A, B, Cc, h, c);
-                    A = An, B = Bn, Cc = Cn;
-                }
-            }
-        } else if (active) {
-            for (uint32_t i = first; i < first + count; i++)
-                test_triangle<STATS>(R, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], h, c);
-        }
-        if (active) active = pop<STRIDE, SW>(nodes4, stk, sp, R, h.best, first, count);
+        if (big_round<STATS, MODE>(tris, pairs, tune, big, active, R, h, T, c))
+            active = pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
     }
 }
 

@@ -31,6 +31,8 @@
 
 #include "mirror.h"
 
+static_assert(MIRROR_BIG_LEAF == (uint32_t)rtfast::BIG, "pair records exist for exactly the big leaves");
+
 // ---------------------------------------------------------------------------------------
 // error state
 // ---------------------------------------------------------------------------------------
@@ -428,30 +430,15 @@ __global__ __launch_bounds__(WAVE) void render_kernel(RenderArgs a) {
 // start a camera sample, trace a segment, shade, end the path on a miss / Russian roulette /
 // the bounce limit, start its next sample -- so a lane only idles once its whole pixel is
 // done.  The per-pixel draw order (u, v, then 4 draws per hit) is the reference's.
-template <int STACK, bool STATS, int WG, int SW>
-__global__ __launch_bounds__(WG) void render_fast_kernel(RenderArgs a) {
-    // dynamic LDS: [hot leaf SoA: 3 x hot_count float4 (WG == BLOCK only)][stack: STACK x SW x WG words]
-    extern __shared__ __attribute__((aligned(16))) char smem[];
+template <int STACK, bool STATS, int MODE>
+__global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
+    __shared__ uint32_t stack_lds[STACK * WAVE];  // one word per entry (rt_fast.h pop)
+    uint32_t* const stk = stack_lds + threadIdx.x;
     const float4* nodes4 = reinterpret_cast<const float4*>(a.nodes);
     const float4* tris = reinterpret_cast<const float4*>(a.tris);
-    const uint32_t hot_count = WG == BLOCK ? a.hot_count : 0u;
-    float4* const hot_lds = reinterpret_cast<float4*>(smem);
-    uint32_t* const stk = reinterpret_cast<uint32_t*>(smem + 48 * (size_t)hot_count) + threadIdx.x;
-    if (WG == BLOCK) {
-        for (uint32_t i = threadIdx.x; i < hot_count; i += BLOCK) {
-            const size_t t = 3 * ((size_t)a.hot_first + i);
-            hot_lds[i] = tris[t];
-            hot_lds[hot_count + i] = tris[t + 1];
-            hot_lds[2 * hot_count + i] = tris[t + 2];
-        }
-        __syncthreads();
-    }
-    rtfast::HotLeaf hot;
-    hot.a = hot_lds, hot.b = hot_lds + hot_count, hot.c = hot_lds + 2 * hot_count;
-    hot.first = a.hot_first, hot.count = hot_count;
-    // WG == BLOCK: one workgroup per 16x16 tile; WG == WAVE: one per 8x8 sub-tile
-    const int k = WG == BLOCK ? (int)blockIdx.x : (int)blockIdx.x >> 2;
-    const int tid = WG == BLOCK ? (int)threadIdx.x : (((int)blockIdx.x & 3) << 6) | (int)threadIdx.x;
+    // one 64-lane workgroup per 8x8 sub-tile: tile k = blockIdx / 4, sub-tile blockIdx % 4
+    const int k = (int)blockIdx.x >> 2;
+    const int tid = (((int)blockIdx.x & 3) << 6) | (int)threadIdx.x;
     const int tile = a.shard_index + k * a.shard_count;
     int lx, ly;
     tile_pixel(tid, &lx, &ly);
@@ -542,7 +529,7 @@ __global__ __launch_bounds__(WG) void render_fast_kernel(RenderArgs a) {
             }
         }
         const rtfast::Ray R = rtfast::make_ray(ro, rd, nd, scene_fast);
-        rtfast::trace<WG, SW, STATS>(nodes4, tris, hot, a.tune, stk, R, h, path, c);
+        rtfast::trace<STATS, MODE>(nodes4, tris, a.pairs, a.tune, stk, R, h, path, c);
         if (!path) continue;
 
         bool end = false;
@@ -718,26 +705,21 @@ hipError_t launch(const RenderArgs& args, int waves, hipStream_t stream) {
     return hipGetLastError();
 }
 
-template <int STACK, bool STATS, int WG, int SW>
-hipError_t launch_fast_wg(const RenderArgs& args, int tiles, hipStream_t stream) {
-    const size_t lds = (WG == BLOCK ? 48 * (size_t)args.hot_count : 0) + (size_t)STACK * SW * WG * 4;
-    static bool attr_set = false;  // allow more than the default 64 KiB of dynamic LDS (160 KiB on gfx950)
-    if (!attr_set) {
-        const hipError_t e = hipFuncSetAttribute((const void*)render_fast_kernel<STACK, STATS, WG, SW>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
-    const int blocks = WG == BLOCK ? tiles : tiles * 4;
-    hipLaunchKernelGGL((render_fast_kernel<STACK, STATS, WG, SW>), dim3(blocks), dim3(WG), lds, stream, args);
+template <int STACK, bool STATS, int MODE>
+hipError_t launch_fast_m(const RenderArgs& args, int tiles, hipStream_t stream) {
+    hipLaunchKernelGGL((render_fast_kernel<STACK, STATS, MODE>), dim3(tiles * 4), dim3(WAVE), 0, stream, args);
     return hipGetLastError();
 }
 
 template <int STACK, bool STATS>
 hipError_t launch_fast_t(const RenderArgs& args, int tiles, hipStream_t stream) {
-    if (args.tune & 4u) return launch_fast_wg<STACK, STATS, BLOCK, 2>(args, tiles, stream);
-    if (args.tune & 8u) return launch_fast_wg<STACK, STATS, WAVE, 2>(args, tiles, stream);
-    return launch_fast_wg<STACK, STATS, WAVE, 1>(args, tiles, stream);
+    if (STATS) return launch_fast_m<STACK, STATS, 2>(args, tiles, stream);  // counts: scalar records
+    // big leaves: packed pairs in the shared-leaf loop, scalar records in cooperative rounds
+    // (MODE 1, measured best); A/B: RT_TUNE bits 4-5 = 2 scalar only, 3 pairs everywhere
+    const uint32_t mode = (args.tune >> 4) & 3u;
+    if (mode == 2) return launch_fast_m<STACK, STATS, 2>(args, tiles, stream);
+    if (mode == 3) return launch_fast_m<STACK, STATS, 0>(args, tiles, stream);
+    return launch_fast_m<STACK, STATS, 1>(args, tiles, stream);
 }
 
 hipError_t launch_fast(const RenderArgs& args, int tiles, int depth, bool stats, hipStream_t s) {
@@ -924,8 +906,7 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     const bool scene_fast = mir.fast;
     static const char* tune = std::getenv("RT_TUNE");  // A/B knobs (RenderArgs::tune)
     a.tune = tune ? (uint32_t)std::strtoul(tune, nullptr, 0) : 0u;
-    a.hot_first = mir.hot_first;
-    a.hot_count = (a.tune & 2u) ? 0u : mir.hot_count;
+    a.pairs = (a.tune & 2u) ? nullptr : (const float4*)mir.pairs;
     static const bool force_ref = std::getenv("RT_FORCE_REFERENCE_LAYOUT") != nullptr;  // A/B switch
     a.tris = force_ref ? nullptr : (const FlatTri*)tris;
     const bool stats = (p->flags & RT_RENDER_STATS) != 0;

@@ -180,6 +180,10 @@ def test_tracers_agree_medium(rt, which, plane_n):
         assert np.array_equal(res["fast"]["frames"][0], res[t]["frames"][0]), t
         assert np.array_equal(res["fast"]["rng"], res[t]["rng"]), t
         assert np.array_equal(res["fast"]["stats"][:7], res[t]["stats"][:7]), t
+    # the production kernel without statistics (pair records, cooperative rounds)
+    g = gpu_render(rt, which, 256, 144, 4, 6, plane_n=plane_n)
+    assert np.array_equal(g["frames"][0], res["ref"]["frames"][0])
+    assert np.array_equal(g["rng"], res["ref"]["rng"])
 
 
 def test_full_size_config2_properties(rt):
