@@ -52,14 +52,20 @@ def algorithmic_bytes(stats, sphere_count, pixels):
     return (32 * nodes + 56 * tris + 32 * sphere_count * seg + 64 * (tacc + sacc) + 36 * tacc + 80 * pixels)
 
 
-def setup_dist():
+def setup_dist(backend="nccl", same_device=False):
+    """One process per GPU (torch.distributed.run sets RANK / LOCAL_RANK / WORLD_SIZE); the
+    "nccl" backend is RCCL on ROCm.  --backend gloo --same-device rehearses the N > 1 path with
+    every rank on GPU 0 (a one-GPU box), staging the gather through host memory."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if same_device else int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     return rank, world
@@ -89,6 +95,21 @@ def cpu_baseline(cfg, sample_rows=None):
             "samples_per_s": round(samples / dt, 1)}
 
 
+def check_unsharded(rt, scene_name, W, H, spp, bounces, frames, final):
+    """Render the same frames on this GPU without sharding (fresh RNG) and compare bit for bit."""
+    scene = rt.Scene()
+    scene.setup(scene_name)
+    scene.set_viewport(W, H)
+    rng = rt.alloc_rng(W * H)
+    rt.init_rng_states(rng, W, H, SEED)
+    scene.upload(rng.data_ptr())
+    bufs = [rt.alloc_surface(W, H) for _ in range(2)]
+    for i in range(frames):
+        rt.render(scene, bufs[i & 1], bufs[(i + 1) & 1], W, H, spp, bounces, i)
+    torch.cuda.synchronize()
+    return bool(torch.equal(rt.surface_view(bufs[(frames - 1) & 1], W), rt.surface_view(final, W)))
+
+
 def load_traffic(cfg):
     """HBM bytes per render launch from a committed PMC summary (profiles/*pmc*.json), if any."""
     best = None
@@ -110,9 +131,13 @@ def main():
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=0, help="rows of the frame the CPU baseline renders (0 = auto)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--same-device", action="store_true", help="every rank on GPU 0 (rehearsal on a one-GPU box)")
+    ap.add_argument("--check", action="store_true",
+                    help="after timing, rank 0 re-renders the same frames unsharded and compares the final frame")
     args = ap.parse_args()
 
-    rank, world = setup_dist()
+    rank, world = setup_dist(args.backend, args.same_device)
     assert world == args.gpus or world == 1, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     rt = G.load_package()
     scene_name, W, H, SPP, BOUNCES, desc = CONFIGS[args.config]
@@ -237,6 +262,8 @@ def main():
             "setup_s": round(setup_s, 2),
             "image_finite": finite,
         }
+        if args.check:
+            result["check_equal"] = check_unsharded(rt, scene_name, W, H, SPP, BOUNCES, n_total, final)
         if world == 1 and not args.no_cpu_baseline:
             auto_rows = {"cfg1": 256, "cfg2": 1080, "cfg3": 64, "cfg4": 540, "cfg5": 1080}[args.config]
             result["cpu_baseline"] = cpu_baseline(args.config, args.cpu_rows or auto_rows)

@@ -60,6 +60,15 @@ def gather_shards(shard, rank, world, out=None):
     import torch
     import torch.distributed as dist
 
+    if shard.is_cuda and dist.get_backend() == "gloo":
+        # rehearsal of the multi-GPU path on one box (gloo gathers host tensors): stage via host
+        got = gather_shards(shard.cpu(), rank, world)
+        if rank != 0:
+            return None
+        if out is None:
+            out = torch.empty((world,) + tuple(shard.shape), dtype=shard.dtype, device=shard.device)
+        out.copy_(got)
+        return out
     if rank == 0:
         if out is None:
             out = torch.empty((world,) + tuple(shard.shape), dtype=shard.dtype, device=shard.device)
