@@ -28,7 +28,7 @@ RT_RENDER_STATS = 1
 TRACERS = {"fast": 0, "ref": 2, "flat": 4}  # rt_render_params.flags
 STAT_NAMES = ("segments", "nodes", "tri_tests", "tri_accepts", "sphere_accepts", "hits", "misses", "",
               "wave_small_iters", "lane_small", "wave_big_tris", "lane_big_tris", "wave_segment_iters",
-              "lane_segments")
+              "lane_segments", "tree_nodes", "tree_tri_tests")
 SCENES = {"bunny": 0, "bunny4": 1, "plane1m": 2}
 
 REFERENCE_SPP = 5      # main_raytracing.cu:166-170 (Release)
@@ -108,8 +108,9 @@ SIGNATURES = {
     "rt_scene_host_arrays": (_SZ, [_P, ctypes.POINTER(_P), ctypes.POINTER(_SZ), ctypes.POINTER(_P),
                                    ctypes.POINTER(_SZ), ctypes.POINTER(_P), ctypes.POINTER(_SZ), ctypes.POINTER(_P)]),
     "rt_scene_bvh_max_depth": (_I, [_P]),
-    "rt_scene_mirror_info": (_I, [_P, ctypes.POINTER(_SZ)]),
-    "rt_scene_mirror_copy": (_I, [_P, _P]),
+    "rt_scene_mirror_info": (_I, [_P, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
+    "rt_scene_mirror_copy": (_I, [_P, _P, _P, _P]),
+    "rt_cluster_cull_host": (_I, [_P, _P, ctypes.c_float, _P]),
     "rt_xorwow_jump_matrix": (_I, [_I, ctypes.POINTER(ctypes.c_uint32)]),
     "rt_xorwow_init_host": (None, [_U32, _U64, _P]),
 }
@@ -222,15 +223,19 @@ class Scene:
     def max_depth(self):
         return lib().rt_scene_bvh_max_depth(self.handle)
 
-    def mirror(self):
-        """The kernel's leaf-ordered triangle mirror built on the host (mirror.h): (N,12) float32
-        records (v0, e1, e2, face id bits, 0, 0)."""
+    def mirror(self, trees=False):
+        """The kernel's triangle mirror built on the host (mirror.h): leaf-ordered (N,12) float32
+        records (v0, e1, e2, face id bits, pair/tree index, flag); with trees=True also the leaf
+        trees: nodes (K,16) and their triangle records (M,12) (leaftree.h)."""
         import numpy as np
-        n = ctypes.c_size_t()
-        _check(lib().rt_scene_mirror_info(self.handle, ctypes.byref(n)), "rt_scene_mirror_info")
-        tris = np.zeros((n.value, 12), dtype=np.float32)
-        _check(lib().rt_scene_mirror_copy(self.handle, tris.ctypes.data), "rt_scene_mirror_copy")
-        return tris
+        n = [ctypes.c_size_t() for _ in range(3)]
+        _check(lib().rt_scene_mirror_info(self.handle, *[ctypes.byref(x) for x in n]), "rt_scene_mirror_info")
+        tris = np.zeros((n[0].value, 12), dtype=np.float32)
+        tree = np.zeros((n[1].value, 16), dtype=np.float32)
+        ltris = np.zeros((n[2].value, 12), dtype=np.float32)
+        _check(lib().rt_scene_mirror_copy(self.handle, tris.ctypes.data, tree.ctypes.data, ltris.ctypes.data),
+               "rt_scene_mirror_copy")
+        return (tris, tree, ltris) if trees else tris
 
     def host_arrays(self):
         """numpy copies of the host arrays: nodes (N,8) f32/u32 view, face indices, vertices, faces."""
@@ -291,6 +296,15 @@ def render(scene, surface, last, width, height, spp, bounces, frame_index=0, sha
         p.stats = stats.data_ptr()
     gpu = scene.gpu if hasattr(scene, "gpu") else ctypes.pointer(scene)  # Scene, or a GPUScene filled by the caller
     _check(lib().rt_render(ctypes.byref(p), ctypes.cast(gpu, ctypes.c_void_p), _stream_ptr(stream)), "rt_render")
+
+
+def cluster_cull_host(origin, nd, best, node):
+    """The render kernel's leaf-tree cull predicate (rt_fast.h cluster_cull) on the host."""
+    import numpy as np
+    o = np.ascontiguousarray(origin, dtype=np.float32)
+    d = np.ascontiguousarray(nd, dtype=np.float32)
+    k = np.ascontiguousarray(node, dtype=np.float32)
+    return bool(lib().rt_cluster_cull_host(o.ctypes.data, d.ctypes.data, float(best), k.ctypes.data))
 
 
 def shard_tiles(width, height, shard_index, shard_count):

@@ -1,0 +1,37 @@
+// leaftree.h -- acceleration inside huge BVH leaves.
+//
+// The reference's midpoint builder (BVH.cpp:60-124) can leave very large leaves -- the 4-bunny
+// scene (BASELINE configs[3]) has one of 12,318 triangles -- and BVHRayHit tests every
+// triangle of a leaf in order.  For such a leaf the mirror also holds a small tree over its
+// triangles; the kernel walks it (rt_fast.h tree_leaf) and skips a subtree only when
+// cluster_cull PROVES that none of its triangles can pass the reference's fp32 triangle test
+// with 0 <= t < closest.  What is tested gives exactly the sequential result: candidates are
+// compared by (t, position in the leaf), and a NaN distance sends the ray back to the
+// sequential loop.
+//
+// Node record, 64 B (pre-order; a node's first child follows it, `skip` = the node after its
+// subtree):
+//   K0 = (box.lo.xyz, E1)      E1   = max over the subtree of max(|e1|_1, |e2|_1)
+//   K1 = (box.hi.xyz, Nmin)    Nmin = min |e2 x e1| (exact, rounded down)
+//   K2 = (axis.xyz, cos)       normal cone: every triangle normal's LINE is within acos(cos)
+//   K3 = (sin, skip, tri_begin, info)         of the fp32 axis; info bit 0 = cullable,
+//                                             bits 8.. = triangle count of a cluster
+// Boxes and cones are rounded outward, so they bound the exact fp32 triangles.  tri_begin
+// indexes the leaf-tree triangle records (FlatTri with C.z = position in the leaf), ~0 for
+// inner nodes.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+struct LeafTreeParams {
+    uint32_t cluster_max = 8;     // triangles per tree leaf
+    double split_angle = 0.6;     // split by normals while the cone half-angle exceeds this (rad)
+    double min_cull_cos = 0.05;   // nodes with a wider cone are never tested (always entered)
+    double big_fraction = 0.25;   // triangles spanning this much of the leaf sit apart, untested
+};
+
+// Appends the tree for `count` FlatTri records (12 floats each) to `nodes` (16 floats per
+// node) and the reordered records to `ltris`; returns the root's node index.
+uint32_t rt_build_leaf_tree(const float* recs, uint32_t count, const LeafTreeParams& prm, std::vector<float>& nodes,
+                            std::vector<float>& ltris);

@@ -2,6 +2,10 @@
 // (see mirror.h for the layout).
 #include "mirror.h"
 
+#include <cstdlib>
+
+#include "leaftree.h"
+
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -35,6 +39,8 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
 
     // walk the tree from the root: depth, filtered-slab range, big leaves
     out->pairs.clear();
+    out->tree.clear();
+    out->ltris.clear();
     out->depth = 0;
     out->fast = true;
     std::vector<uint32_t> big;
@@ -71,6 +77,18 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
         uint32_t pf;
         std::memcpy(&pf, &lead[11], 4);
         if (pf) continue;  // two nodes sharing one leaf range
+        static const uint32_t tree_min = [] {
+            const char* e = std::getenv("RT_LEAF_TREE_MIN");  // tuning
+            return e ? (uint32_t)std::strtoul(e, nullptr, 0) : MIRROR_TREE_LEAF;
+        }();
+        if (nd.prim_count >= tree_min) {
+            po = rt_build_leaf_tree(&out->tris[(size_t)nd.first_index * 12], nd.prim_count, LeafTreeParams{}, out->tree,
+                                    out->ltris);
+            pf = 2;
+            std::memcpy(&lead[10], &po, 4);
+            std::memcpy(&lead[11], &pf, 4);
+            continue;
+        }
         po = (uint32_t)(out->pairs.size() / 20);
         pf = 1;
         std::memcpy(&lead[10], &po, 4);
@@ -112,17 +130,21 @@ void release(Entry& e) {
 }  // namespace
 
 int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owned, uint64_t fingerprint) {
-    const size_t nt = m.tris.size() * 4, np = m.pairs.size() * 4;
+    const size_t nt = m.tris.size() * 4, np = m.pairs.size() * 4, nk = m.tree.size() * 4, nl = m.ltris.size() * 4;
     void* block = nullptr;
-    if (rt_malloc(&block, nt + np + 64) != 0) return -1;
+    if (rt_malloc(&block, nt + np + nk + nl + 64) != 0) return -1;
     char* b = static_cast<char*>(block);
-    if ((nt && rt_memcpy_h2d(b, m.tris.data(), nt) != 0) || (np && rt_memcpy_h2d(b + nt, m.pairs.data(), np) != 0)) {
+    if ((nt && rt_memcpy_h2d(b, m.tris.data(), nt) != 0) || (np && rt_memcpy_h2d(b + nt, m.pairs.data(), np) != 0) ||
+        (nk && rt_memcpy_h2d(b + nt + np, m.tree.data(), nk) != 0) ||
+        (nl && rt_memcpy_h2d(b + nt + np + nk, m.ltris.data(), nl) != 0)) {
         rt_free(block);
         return -1;
     }
     Entry e{s->gpu_bvh_face_indices, s->gpu_vertices, s->gpu_faces, block, {}};
     e.dev.tris = b;
     e.dev.pairs = np ? b + nt : nullptr;
+    e.dev.tree = nk ? b + nt + np : nullptr;
+    e.dev.ltris = nl ? b + nt + np + nk : nullptr;
     e.dev.depth = m.depth;
     e.dev.fast = m.fast;
     e.dev.owned = owned;

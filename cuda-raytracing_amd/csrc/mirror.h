@@ -12,6 +12,8 @@
 //           (v0z, e1x), (e1y, e1z), (e2x, e2y), (e2z_a, e2z_b, face_a, face_b) -- the operand
 //           layout of packed fp32 instructions; an odd leaf ends with an all-zero triangle.  The
 //           leaf's first tris record holds po = its first pair, pf = 1 (0 for other leaves);
+//  * tree / ltris  for leaves of at least MIRROR_TREE_LEAF triangles, a leaf tree instead
+//           (leaftree.h): the first record holds po = the root node, pf = 2;
 //  * depth  the deepest leaf (sizes the traversal stack) and whether every node bound lies in
 //           the range where the filtered slab test is proven (rt_fast.h).
 #pragma once
@@ -22,11 +24,14 @@
 
 #include "rt_abi.h"
 
-constexpr uint32_t MIRROR_BIG_LEAF = 8;  // leaves above this get pair records (== rtfast::BIG)
+constexpr uint32_t MIRROR_BIG_LEAF = 8;     // leaves above this get pair records (== rtfast::BIG)
+constexpr uint32_t MIRROR_TREE_LEAF = 1024;  // ... and leaves this large a leaf tree (leaftree.h) instead
 
 struct MirrorHost {
     std::vector<float> tris;      // 12 floats per record
     std::vector<float> pairs;     // 20 floats per pair
+    std::vector<float> tree;      // 16 floats per leaf-tree node
+    std::vector<float> ltris;     // 12 floats per leaf-tree triangle record
     int depth = 0;                // deepest leaf (root = 0) reachable from node 0
     bool fast = true;             // node bounds inside the filtered-slab range (rt_fast.h)
 };
@@ -42,6 +47,8 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
 struct MirrorDevice {
     const void* tris = nullptr;
     const void* pairs = nullptr;
+    const void* tree = nullptr;
+    const void* ltris = nullptr;
     int depth = -1;
     bool fast = false;
     bool owned = true;         // built by rt_scene_upload, which forgets it before freeing the arrays

@@ -44,13 +44,16 @@ struct RenderArgs {
     unsigned long long* seg_counter;
     int scene_fast;  // all node bounds inside the filtered-slab range (rt_fast.h)
     const float4* pairs;  // big leaves' triangles in packed pairs (mirror.h) or null
+    const float4* tree;   // leaf trees of huge leaves (leaftree.h) or null
+    const float4* ltris;  // their triangle records
     uint32_t tune;  // A/B knobs (RT_TUNE, rt_render): bit0 no cooperative leaf rounds, bit1 no pair
-                    // records, bits 4-5 big-leaf mode (rt_kernel.hip launch_fast_t)
+                    // records, bit2 no leaf trees, bits 4-5 big-leaf mode (rt_kernel.hip launch_fast_t)
 };
 
 struct Counters {
     unsigned long long seg = 0, node = 0, tri = 0, tacc = 0, sacc = 0, hit = 0, miss = 0;
     unsigned long long w_small = 0, l_small = 0, w_big = 0, l_big = 0, w_seg = 0, l_seg = 0;
+    unsigned long long ktest = 0, ktri = 0;  // leaf-tree node visits / triangle tests
 };
 
 __device__ __forceinline__ rtm::f3 ld3(const float* p) { return rtm::f3{p[0], p[1], p[2]}; }

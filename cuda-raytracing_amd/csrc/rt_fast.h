@@ -475,6 +475,136 @@ __device__ __forceinline__ void coop_leaf_scalar(const float4* tris, unsigned lo
 
 // BVHRayHit for one lane (`live` = the lane has a segment to trace).  Every lane of the wave
 // must call it (it synchronises big leaves across the wave).  STRIDE: the stack's lane stride.
+// ---------------------------------------------------------------------------------------
+// Leaf trees (leaftree.h).  BVHRayHit tests a leaf's triangles in order and keeps a triangle
+// iff `!(t >= best || t < 0)`; for a finite `best` and finite distances the result is the
+// first index attaining the minimum distance below the entry `best`.  tree_leaf computes
+// exactly that -- candidates compared by (t, index) -- testing only the clusters cluster_cull
+// cannot exclude, and redoes the leaf sequentially when a NaN shows up.
+// ---------------------------------------------------------------------------------------
+struct LeafBest {
+    float t;       // running minimum (starts at the entry `best`)
+    uint32_t j;    // its position inside the leaf (valid when found)
+    uint32_t id;   // face id
+    float bx, by;
+    bool found, nan;
+};
+
+// glm::intersectRayTriangle as in test_triangle, candidate kept by (t, index).
+__device__ __forceinline__ void leaf_candidate(const Ray& R, float4 A, float4 B, float4 Cc, LeafBest& L) {
+    const f3 e1 = rtm::mk(A.w, B.x, B.y), e2 = rtm::mk(B.z, B.w, Cc.x);
+    const f3 p = rtm::cross(R.nd, e2);
+    const float det = rtm::dot(e1, p);
+    const f3 dist = rtm::sub(R.o, rtm::mk(A.x, A.y, A.z));
+    const float u = rtm::dot(dist, p);
+    const f3 perp = rtm::cross(dist, e1);
+    const float v = rtm::dot(R.nd, perp);
+    if (tri_ok(det, u, v, u + v)) {
+        const float inv_det = 1.0f / det;
+        const float t = rtm::dot(e2, perp) * inv_det;
+        const uint32_t j = __float_as_uint(Cc.z);
+        L.nan = L.nan || (t != t);
+        if (t >= 0.0f && (t < L.t || (t == L.t && L.found && j < L.j))) {
+            L.t = t, L.j = j, L.id = __float_as_uint(Cc.y);
+            L.bx = u * inv_det, L.by = v * inv_det;
+            L.found = true;
+        }
+    }
+}
+
+// true => no triangle under the node can pass the fp32 test with 0 <= t < best for this ray.
+//
+// Why (U = 2^-24; every error term is bounded with the standard error model of the glm
+// operation order, constants rounded up and then doubled): if the computed test accepts
+// triangle (v0, e1, e2), then with D = |det| (exact) the exact barycentrics of the line/plane
+// intersection X violate [b1 >= 0, b2 >= 0, b1 + b2 <= 1] by at most
+//   d = 2U + U*N1*(24.1*|o - v0|_1*E1 + 5.1*E1^2)/D,   N1 = |nd|_1 <= 1.7321,
+// so X lies within r = 4*d*E1 of the triangle, and X's exact ray parameter lies within Et of the
+// computed t (once D >= 4x the det error, required below).  D >= Dlb comes from the node's
+// normal cone (K2, K3.x) and Nmin, |o - v0|_1 <= Dist1 from its box.  The slab test then checks
+// the ray segment [-Et, min(best, Tmax) + Et] against the box grown by r, with a margin m
+// (2^-16 relative) that absorbs the rounding of the test itself.  Rays outside the filtered
+// range (R.fast false) are never culled.  tests/test_leaf_tree.py checks the bound on the host.
+RT_HD bool cluster_cull(const Ray& R, f3 rnd, float best, float4 K0, float4 K1, float4 K2, float4 K3) {
+    const float U = 0x1p-24f;
+    if (!(best == best)) return false;
+    const float E1 = K0.w, Nmin = K1.w;
+    const float dota = fabsf(R.nd.x * K2.x + R.nd.y * K2.y + R.nd.z * K2.z);
+    const float ca = fminf(fmaxf(dota * (1.0f - 0x1p-20f) - 4.0f * U, 0.0f), 1.0f);  // <= cos(angle(nd, axis))
+    const float sa = sqrtf(fmaxf(1.0f - ca * ca, 0.0f) + 2.0f * U) * (1.0f + 0x1p-20f);  // >= its sine
+    const float dlb = Nmin * ((ca * K2.w - sa * K3.x) - 4.0f * U) * (1.0f - 0x1p-20f);  // <= min |det|
+    if (!(dlb > 36.0f * U * E1 * E1)) return false;
+    const float g = E1 / dlb * (1.0f + 0x1p-20f);
+    const float dx = fmaxf(fabsf(R.o.x - K0.x), fabsf(R.o.x - K1.x));
+    const float dy = fmaxf(fabsf(R.o.y - K0.y), fabsf(R.o.y - K1.y));
+    const float dz = fmaxf(fabsf(R.o.z - K0.z), fabsf(R.o.z - K1.z));
+    const float dist1 = ((dx + dy) + dz) * (1.0f + 0x1p-20f);
+    const float r = U * E1 * (8.0f + g * (168.0f * dist1 + 36.0f * E1)) * (1.0f + 0x1p-18f) + 0x1p-100f;
+    const float tmax = (dist1 + r) * (1.0f + 0x1p-18f);
+    const float et = U * tmax * (53.0f * E1 * g + 8.125f) * (1.0f + 0x1p-18f);
+    const float send = fminf(best, tmax);
+    const float m = 0x1p-16f * (send + et) + 0x1p-100f;
+    const float s0 = -(et + m), s1 = send + et + m;
+    const float bmax = fmaxf(fmaxf(fmaxf(fabsf(K0.x), fabsf(K1.x)), fmaxf(fabsf(K0.y), fabsf(K1.y))),
+                             fmaxf(fabsf(K0.z), fabsf(K1.z)));
+    const float ex0 = (r + 1.01f * m) * (1.0f + 0x1p-20f);
+    const float ex = ex0 + 0x1p-20f * (bmax + ex0);
+    const float tx1 = ((K0.x - ex) - R.o.x) * rnd.x, tx2 = ((K1.x + ex) - R.o.x) * rnd.x;
+    const float ty1 = ((K0.y - ex) - R.o.y) * rnd.y, ty2 = ((K1.y + ex) - R.o.y) * rnd.y;
+    const float tz1 = ((K0.z - ex) - R.o.z) * rnd.z, tz2 = ((K1.z + ex) - R.o.z) * rnd.z;
+    const float lo = fmaxf(s0, fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2)));
+    const float hi = fminf(s1, fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2)));
+    return lo > hi;
+}
+
+// Leaf [f0, f0 + c0) through its tree (root `root`), this lane alone (stackless: pre-order
+// with skip pointers).
+template <bool STATS, class C>
+__device__ __forceinline__ void tree_leaf(const float4* tris, const float4* tree, const float4* ltris, uint32_t root,
+                                          uint32_t f0, uint32_t c0, const Ray& R, Hit& h, C& c) {
+    if (STATS) c.tri += c0;  // the reference's work (tri_tests); node visits / tests run below
+    LeafBest L;
+    L.t = h.best, L.j = 0, L.id = 0, L.bx = 0.0f, L.by = 0.0f, L.found = false;
+    L.nan = !(h.best == h.best);
+    const bool cull_ok = R.fast;
+    const f3 rnd = cull_ok ? rtm::mk(1.0f / R.nd.x, 1.0f / R.nd.y, 1.0f / R.nd.z) : rtm::mk(0.0f, 0.0f, 0.0f);
+    const uint32_t end = __float_as_uint(tree[4 * (size_t)root + 3].y);
+    uint32_t k = root;
+    while (k < end) {
+        const float4* kp = tree + 4 * (size_t)k;
+        const float4 K3 = kp[3];
+        const uint32_t skip = __float_as_uint(K3.y), info = __float_as_uint(K3.w);
+        if (STATS) c.ktest++;
+        if (cull_ok && !L.nan && (info & 1u) && cluster_cull(R, rnd, L.t, kp[0], kp[1], kp[2], K3)) {
+            k = skip;
+            continue;
+        }
+        const uint32_t b = __float_as_uint(K3.z);
+        if (b != 0xffffffffu) {
+            const uint32_t n = info >> 8;
+            if (STATS) c.ktri += n;
+            for (uint32_t i = b; i < b + n; i++) leaf_candidate(R, ltris[3 * i], ltris[3 * i + 1], ltris[3 * i + 2], L);
+            k = skip;
+        } else {
+            k++;
+        }
+    }
+    if (L.nan) {
+        for (uint32_t i = f0; i < f0 + c0; i++) {
+            float t, x, y;
+            bool dummy = false;
+            const float4 A = tris[3 * i], B = tris[3 * i + 1], Cc = tris[3 * i + 2];
+            if (tri_accept(R.o, R.nd, A, B, Cc, h.best, &t, &x, &y, &dummy)) {
+                h.best = t, h.kind = 2, h.bx = x, h.by = y;
+                h.id = __float_as_uint(Cc.y);
+            }
+        }
+    } else if (L.found) {
+        h.best = L.t, h.kind = 2, h.id = L.id, h.bx = L.bx, h.by = L.by;
+        if (STATS) c.tacc++;
+    }
+}
+
 // Traversal state of one lane between steps: the node (or leaf) it is at and its stack depth.
 struct Trav {
     uint32_t first, count;
@@ -512,8 +642,23 @@ __device__ __forceinline__ bool small_step(const float4* nodes4, const float4* t
 // lane is at that leaf, or each lane alone otherwise (MODE: see trace).  Returns whether this
 // lane ran its leaf (it then pops; the others keep waiting).
 template <bool STATS, int MODE, class C>
-__device__ __forceinline__ bool big_round(const float4* tris, const float4* pairs, uint32_t tune, unsigned long long big,
-                                          bool waiting, const Ray& R, Hit& h, const Trav& T, C& c) {
+__device__ __forceinline__ bool big_round(const float4* tris, const float4* pairs, const float4* tree,
+                                          const float4* ltris, uint32_t tune, unsigned long long big, bool waiting,
+                                          const Ray& R, Hit& h, const Trav& T, C& c) {
+    if ((MODE & 4) && tree) {  // MODE bit 2: the scene has leaf trees
+        // lanes at leaves with a leaf tree (mirror.h: lead record pf == 2) walk it on their own
+        bool at_tree = false;
+        uint32_t root = 0;
+        if (waiting) {
+            const float4 lead = tris[3 * (size_t)T.first + 2];
+            at_tree = __float_as_uint(lead.w) == 2u;
+            root = __float_as_uint(lead.z);
+        }
+        if (__ballot(at_tree)) {
+            if (at_tree) tree_leaf<STATS>(tris, tree, ltris, root, T.first, T.count, R, h, c);
+            return at_tree;
+        }
+    }
     const int l0 = __ffsll((long long)big) - 1;
     const uint32_t f0 = __builtin_amdgcn_readlane(T.first, l0);
     const uint32_t c0 = __builtin_amdgcn_readlane(T.count, l0);
@@ -527,15 +672,15 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
         // the first record of a big leaf says where its pairs are (mirror.h)
         const f4v lead = ((ConstF4)(tris + 3 * (size_t)f0))[2];
         const uint32_t k = (uint32_t)__popcll(big);
-        if (!STATS && MODE < 2 && pairs && __float_as_uint(lead.w) != 0u) {
+        if (!STATS && (MODE & 3) < 2 && pairs && __float_as_uint(lead.w) == 1u) {
             const float4* lp = pairs + 5 * (size_t)__float_as_uint(lead.z);
             const uint32_t np = (c0 + 1u) / 2u, chunks = (np + 63u) / 64u;
             // cost model (VALU instructions per pair ~40): cooperative ~ k * (40 * chunks + 60),
             // shared-leaf ~ 40 * np for all waiting lanes at once
             const uint32_t cchunks = (c0 + 63u) / 64u;
-            if (MODE == 0 && (tune & 1u) == 0 && k * (40u * chunks + 60u) < 40u * np) {
+            if ((MODE & 3) == 0 && (tune & 1u) == 0 && k * (40u * chunks + 60u) < 40u * np) {
                 coop_leaf(tris, lp, big, f0, c0, R, h);
-            } else if (MODE == 1 && (tune & 1u) == 0 && k * (60u * cchunks + 50u) < 40u * np) {
+            } else if ((MODE & 3) == 1 && (tune & 1u) == 0 && k * (60u * cchunks + 50u) < 40u * np) {
                 coop_leaf_scalar(tris, big, f0, c0, R, h);
             } else {
                 ConstF4 ps = (ConstF4)lp;
@@ -570,11 +715,14 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
 
 // BVHRayHit for one lane (`live` = the lane has a segment to trace), every lane of the wave
 // calling.  Small steps run while any lane has one; big leaves wait until every lane is done
-// or waiting at one.  MODE 0: big leaves through pair records (shared-leaf loop and cooperative
-// rounds); 1: pairs in the shared-leaf loop, scalar cooperative rounds; 2: scalar records only.
+// or waiting at one.  MODE & 3 -- 0: big leaves through pair records (shared-leaf loop and
+// cooperative rounds); 1: pairs in the shared-leaf loop, scalar cooperative rounds; 2: scalar
+// records only.  MODE & 4: leaves with a leaf tree walk it (a statistics frame then counts the
+// reference's triangle tests plus the tree's own work).
 template <bool STATS, int MODE, class C>
-__device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, const float4* pairs, uint32_t tune,
-                                      uint32_t* stk, const Ray& R, Hit& h, bool live, C& c) {
+__device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, const float4* pairs,
+                                      const float4* tree, const float4* ltris, uint32_t tune, uint32_t* stk,
+                                      const Ray& R, Hit& h, bool live, C& c) {
     Trav T{0, 0, 0};
     bool active = live && trav_begin<STATS>(nodes4, R, h, T, c);
     for (;;) {
@@ -589,7 +737,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
         }
         const unsigned long long big = __ballot(active);
         if (!big) break;
-        if (big_round<STATS, MODE>(tris, pairs, tune, big, active, R, h, T, c))
+        if (big_round<STATS, MODE>(tris, pairs, tree, ltris, tune, big, active, R, h, T, c))
             active = pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
     }
 }

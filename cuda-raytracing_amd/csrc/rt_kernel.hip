@@ -529,7 +529,7 @@ __global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
             }
         }
         const rtfast::Ray R = rtfast::make_ray(ro, rd, nd, scene_fast);
-        rtfast::trace<STATS, MODE>(nodes4, tris, a.pairs, a.tune, stk, R, h, path, c);
+        rtfast::trace<STATS, MODE>(nodes4, tris, a.pairs, a.tree, a.ltris, a.tune, stk, R, h, path, c);
         if (!path) continue;
 
         bool end = false;
@@ -617,6 +617,8 @@ __global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
         atomicAdd(a.stats + RT_STAT_LANE_BIG_TRIS, c.l_big);
         atomicAdd(a.stats + RT_STAT_WAVE_SEGMENT_ITERS, c.w_seg);
         atomicAdd(a.stats + RT_STAT_LANE_SEGMENTS, c.l_seg);
+        atomicAdd(a.stats + RT_STAT_TREE_NODES, c.ktest);
+        atomicAdd(a.stats + RT_STAT_TREE_TRI_TESTS, c.ktri);
     }
 }
 
@@ -713,9 +715,13 @@ hipError_t launch_fast_m(const RenderArgs& args, int tiles, hipStream_t stream) 
 
 template <int STACK, bool STATS>
 hipError_t launch_fast_t(const RenderArgs& args, int tiles, hipStream_t stream) {
-    if (STATS) return launch_fast_m<STACK, STATS, 2>(args, tiles, stream);  // counts: scalar records
+    // statistics: the reference's work on scalar records (RT_TUNE bit 7: through the leaf trees)
+    if (STATS) return (args.tree && (args.tune & 128u)) ? launch_fast_m<STACK, STATS, 6>(args, tiles, stream)
+                                                        : launch_fast_m<STACK, STATS, 2>(args, tiles, stream);
     // big leaves: packed pairs in the shared-leaf loop, scalar records in cooperative rounds
-    // (MODE 1, measured best); A/B: RT_TUNE bits 4-5 = 2 scalar only, 3 pairs everywhere
+    // (MODE 1, measured best), leaf trees compiled in only for scenes that have them (MODE 5);
+    // A/B: RT_TUNE bits 4-5 = 2 scalar only, 3 pairs everywhere
+    if (args.tree) return launch_fast_m<STACK, STATS, 5>(args, tiles, stream);
     const uint32_t mode = (args.tune >> 4) & 3u;
     if (mode == 2) return launch_fast_m<STACK, STATS, 2>(args, tiles, stream);
     if (mode == 3) return launch_fast_m<STACK, STATS, 0>(args, tiles, stream);
@@ -907,6 +913,8 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     static const char* tune = std::getenv("RT_TUNE");  // A/B knobs (RenderArgs::tune)
     a.tune = tune ? (uint32_t)std::strtoul(tune, nullptr, 0) : 0u;
     a.pairs = (a.tune & 2u) ? nullptr : (const float4*)mir.pairs;
+    a.tree = (a.tune & 4u) ? nullptr : (const float4*)mir.tree;
+    a.ltris = (const float4*)mir.ltris;
     static const bool force_ref = std::getenv("RT_FORCE_REFERENCE_LAYOUT") != nullptr;  // A/B switch
     a.tris = force_ref ? nullptr : (const FlatTri*)tris;
     const bool stats = (p->flags & RT_RENDER_STATS) != 0;
@@ -988,3 +996,19 @@ extern "C" void init_rng(uint32_t thread_block_count, uint32_t thread_block_size
     if (check(hipGetLastError(), "init_rng_kernel launch")) std::printf("(init_rng) failed: %s\n", rt_last_error());
 }
 
+
+// Diagnostics: the leaf-tree cull predicate of the render kernel, evaluated on the host by the
+// same code (tests/test_leaf_tree.py).
+extern "C" int rt_cluster_cull_host(const float origin[3], const float nd[3], float best, const float node[16]) {
+    rtfast::Ray R;
+    R.o = rtm::mk(origin[0], origin[1], origin[2]);
+    R.nd = rtm::mk(nd[0], nd[1], nd[2]);
+    R.d = R.nd;
+    R.r = rtm::mk(1.0f / nd[0], 1.0f / nd[1], 1.0f / nd[2]);
+    R.fast = true;
+    const float4 K0 = make_float4(node[0], node[1], node[2], node[3]);
+    const float4 K1 = make_float4(node[4], node[5], node[6], node[7]);
+    const float4 K2 = make_float4(node[8], node[9], node[10], node[11]);
+    const float4 K3 = make_float4(node[12], node[13], node[14], node[15]);
+    return rtfast::cluster_cull(R, R.r, best, K0, K1, K2, K3) ? 1 : 0;
+}

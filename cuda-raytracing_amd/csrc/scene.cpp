@@ -626,16 +626,20 @@ static int host_mirror(rt_scene* s, MirrorHost* m) {
     }
     return 0;
 }
-int rt_scene_mirror_info(rt_scene* s, size_t* tri_records) {
+int rt_scene_mirror_info(rt_scene* s, size_t* tri_records, size_t* tree_nodes, size_t* tree_tri_records) {
     MirrorHost m;
     if (host_mirror(s, &m) != 0) return -1;
     *tri_records = m.tris.size() / 12;
+    *tree_nodes = m.tree.size() / 16;
+    *tree_tri_records = m.ltris.size() / 12;
     return 0;
 }
-int rt_scene_mirror_copy(rt_scene* s, float* tris) {
+int rt_scene_mirror_copy(rt_scene* s, float* tris, float* tree, float* tree_tris) {
     MirrorHost m;
     if (host_mirror(s, &m) != 0) return -1;
     std::copy(m.tris.begin(), m.tris.end(), tris);
+    std::copy(m.tree.begin(), m.tree.end(), tree);
+    std::copy(m.ltris.begin(), m.ltris.end(), tree_tris);
     return 0;
 }
 void rt_scene_build(rt_scene* s) { s->scene.BuildHost(); }

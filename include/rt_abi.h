@@ -187,6 +187,8 @@ enum {
     RT_STAT_LANE_BIG_TRIS = 11,
     RT_STAT_WAVE_SEGMENT_ITERS = 12,/* segment-loop iterations */
     RT_STAT_LANE_SEGMENTS = 13,
+    RT_STAT_TREE_NODES = 14,        /* leaf-tree nodes visited (leaftree.h; statistics frames with RT_TUNE bit 7) */
+    RT_STAT_TREE_TRI_TESTS = 15,    /* triangle tests run inside leaf trees */
     RT_STAT_COUNT = 16
 };
 
@@ -267,11 +269,14 @@ size_t rt_scene_host_arrays(const rt_scene* scene, const GPUBVHNode** nodes, siz
                             size_t* vertex_count, const GPUFace** faces);
 int rt_scene_bvh_max_depth(const rt_scene* scene);
 
-/* Diagnostics for the tests: the kernel's private leaf-ordered triangle mirror
-   (cuda-raytracing_amd/csrc/mirror.h, 12 floats per record) built on the host from the scene's
-   host arrays.  Returns 0, or -1 with rt_last_error(). */
-int rt_scene_mirror_info(rt_scene* scene, size_t* tri_records);
-int rt_scene_mirror_copy(rt_scene* scene, float* tris);
+/* Diagnostics for the tests: the kernel's private triangle mirror (cuda-raytracing_amd/csrc/
+   mirror.h: leaf-ordered records, 12 floats; leaf-tree nodes, 16 floats; leaf-tree triangle
+   records, 12 floats) built on the host from the scene's host arrays, and the render kernel's
+   leaf-tree cull predicate (rt_fast.h cluster_cull) evaluated on the host by the same code.
+   Returns 0 (cull: 1 = culled), or -1 with rt_last_error(). */
+int rt_scene_mirror_info(rt_scene* scene, size_t* tri_records, size_t* tree_nodes, size_t* tree_tri_records);
+int rt_scene_mirror_copy(rt_scene* scene, float* tris, float* tree, float* tree_tris);
+int rt_cluster_cull_host(const float origin[3], const float nd[3], float best, const float node[16]);
 
 /* XORWOW jump matrix A^(4^k * 2^67) (k < 32) as 800 uint32 words in rocrand's layout
  * m[i*160 + j*5 + w] (input word i, bit j, output word w).  For tests. */
