@@ -170,7 +170,7 @@ def main():
 
     # --- exact traversal counts of one frame (stats kernel variant) on a copy of the RNG state
     rng_saved = rng.clone()
-    stats = torch.zeros(16, dtype=torch.int64, device=dev)
+    stats = torch.zeros(24, dtype=torch.int64, device=dev)
     if sharded:
         rt.render(scene, None, bufs[1], W, H, SPP, BOUNCES, 0, rank, world, out_shard=bufs[0], stats=stats)
     else:

@@ -431,9 +431,7 @@ __global__ __launch_bounds__(WAVE) void render_kernel(RenderArgs a) {
 // the bounce limit, start its next sample -- so a lane only idles once its whole pixel is
 // done.  The per-pixel draw order (u, v, then 4 draws per hit) is the reference's.
 template <int STACK, bool STATS, int MODE>
-__global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
-    __shared__ uint32_t stack_lds[STACK * WAVE];  // one word per entry (rt_fast.h pop)
-    uint32_t* const stk = stack_lds + threadIdx.x;
+__device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* const stk) {
     const float4* nodes4 = reinterpret_cast<const float4*>(a.nodes);
     const float4* tris = reinterpret_cast<const float4*>(a.tris);
     // one 64-lane workgroup per 8x8 sub-tile: tile k = blockIdx / 4, sub-tile blockIdx % 4
@@ -457,6 +455,7 @@ __global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
     bool path = false;
     rtm::f3 ro = cam_o, rd = cam_o, color = rtm::mk(0, 0, 0), thr = rtm::mk(1, 1, 1);
     const bool scene_fast = a.scene_fast != 0;
+    const unsigned long long t_start = (MODE & 8) ? __builtin_amdgcn_s_memtime() : 0;
 
     for (;;) {
         if (pixel && !path) {
@@ -603,6 +602,14 @@ __global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
         if ((threadIdx.x & 63) == 0) atomicAdd(a.seg_counter, v);
     }
+    if ((MODE & 8) && a.stats && threadIdx.x == 0) {  // timing frame: per-wave phase clocks
+        atomicAdd(a.stats + RT_STAT_CYCLES_SMALL, c.cy_small);
+        atomicAdd(a.stats + RT_STAT_CYCLES_BIG, c.cy_big);
+        atomicAdd(a.stats + RT_STAT_CYCLES_TOTAL, __builtin_amdgcn_s_memtime() - t_start);
+        atomicAdd(a.stats + RT_STAT_ROUNDS_COOP, c.r_coop);
+        atomicAdd(a.stats + RT_STAT_ROUNDS_SHARED, c.r_shared);
+        atomicAdd(a.stats + RT_STAT_COOP_RAYS, c.coop_rays);
+    }
     if (STATS) {
         atomicAdd(a.stats + RT_STAT_SEGMENTS, c.seg);
         atomicAdd(a.stats + RT_STAT_NODES, c.node);
@@ -620,6 +627,25 @@ __global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
         atomicAdd(a.stats + RT_STAT_TREE_NODES, c.ktest);
         atomicAdd(a.stats + RT_STAT_TREE_TRI_TESTS, c.ktri);
     }
+}
+
+// The production kernel.  The _w5 / _w6 variants ask the compiler for 5 / 6 waves per SIMD
+// (fewer registers, some spilled) -- an occupancy / spill trade-off (RT_TUNE bits 9-10:
+// 0 = _w5, the default; 1 = unconstrained; 2 = _w6).
+template <int STACK, bool STATS, int MODE>
+__global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
+    __shared__ uint32_t stack_lds[STACK * WAVE];  // one word per entry (rt_fast.h pop)
+    render_fast_body<STACK, STATS, MODE>(a, stack_lds + threadIdx.x);
+}
+template <int STACK, bool STATS, int MODE>
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(5))) void render_fast_kernel_w5(RenderArgs a) {
+    __shared__ uint32_t stack_lds[STACK * WAVE];
+    render_fast_body<STACK, STATS, MODE>(a, stack_lds + threadIdx.x);
+}
+template <int STACK, bool STATS, int MODE>
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(6))) void render_fast_kernel_w6(RenderArgs a) {
+    __shared__ uint32_t stack_lds[STACK * WAVE];
+    render_fast_body<STACK, STATS, MODE>(a, stack_lds + threadIdx.x);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -709,13 +735,22 @@ hipError_t launch(const RenderArgs& args, int waves, hipStream_t stream) {
 
 template <int STACK, bool STATS, int MODE>
 hipError_t launch_fast_m(const RenderArgs& args, int tiles, hipStream_t stream) {
-    hipLaunchKernelGGL((render_fast_kernel<STACK, STATS, MODE>), dim3(tiles * 4), dim3(WAVE), 0, stream, args);
+    // default: 5 waves per SIMD (96 VGPRs, a few cold spills; 4 % faster than the compiler's 126)
+    const uint32_t occ = (args.tune >> 9) & 3u;
+    if (!STATS && occ == 0)
+        hipLaunchKernelGGL((render_fast_kernel_w5<STACK, STATS, MODE>), dim3(tiles * 4), dim3(WAVE), 0, stream, args);
+    else if (!STATS && occ == 2)
+        hipLaunchKernelGGL((render_fast_kernel_w6<STACK, STATS, MODE>), dim3(tiles * 4), dim3(WAVE), 0, stream, args);
+    else
+        hipLaunchKernelGGL((render_fast_kernel<STACK, STATS, MODE>), dim3(tiles * 4), dim3(WAVE), 0, stream, args);
     return hipGetLastError();
 }
 
 template <int STACK, bool STATS>
 hipError_t launch_fast_t(const RenderArgs& args, int tiles, hipStream_t stream) {
-    // statistics: the reference's work on scalar records (RT_TUNE bit 7: through the leaf trees)
+    // statistics: the reference's work on scalar records (RT_TUNE bit 7: through the leaf trees);
+    // RT_TUNE bit 8: a timing frame of the production kernel instead (phase clocks, no counts)
+    if (STATS && (args.tune & 256u)) return launch_fast_m<STACK, false, 9>(args, tiles, stream);
     if (STATS) return (args.tree && (args.tune & 128u)) ? launch_fast_m<STACK, STATS, 6>(args, tiles, stream)
                                                         : launch_fast_m<STACK, STATS, 2>(args, tiles, stream);
     // big leaves: packed pairs in the shared-leaf loop, scalar records in cooperative rounds

@@ -189,7 +189,13 @@ enum {
     RT_STAT_LANE_SEGMENTS = 13,
     RT_STAT_TREE_NODES = 14,        /* leaf-tree nodes visited (leaftree.h; statistics frames with RT_TUNE bit 7) */
     RT_STAT_TREE_TRI_TESTS = 15,    /* triangle tests run inside leaf trees */
-    RT_STAT_COUNT = 16
+    RT_STAT_CYCLES_SMALL = 16,      /* RT_TUNE bit 8 timing frames: wave clock cycles in small steps */
+    RT_STAT_CYCLES_BIG = 17,        /* ... in big-leaf rounds */
+    RT_STAT_CYCLES_TOTAL = 18,      /* ... in the whole kernel */
+    RT_STAT_ROUNDS_COOP = 19,       /* cooperative big-leaf rounds */
+    RT_STAT_ROUNDS_SHARED = 20,     /* shared-leaf (pair / scalar-load) rounds */
+    RT_STAT_COOP_RAYS = 21,         /* rays run through cooperative rounds */
+    RT_STAT_COUNT = 24
 };
 
 /* Render on `stream` (a hipStream_t, NULL = null stream).  Returns 0 or an error code. */
