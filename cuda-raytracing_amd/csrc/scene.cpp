@@ -374,6 +374,21 @@ static AiMat ai_mul(const AiMat& a, const AiMat& m) {
     return o;
 }
 
+// aiMatrix4x4::RotationX(-(float)M_PI / 2) as the accumulated root transform, times the
+// (identity) root and mesh node transforms, then convert_matrix (transpose into glm).
+mat4 ImporterRootTransform() {
+    const float a = -3.14159265358979323846f / 2;
+    AiMat rx = ai_identity();
+    rx.r[1][1] = rx.r[2][2] = rth::hcos(a);
+    rx.r[2][1] = rth::hsin(a);
+    rx.r[1][2] = -rx.r[2][1];
+    const AiMat acc = ai_mul(ai_mul(rx, ai_identity()), ai_identity());
+    mat4 t;
+    for (int c = 0; c < 4; c++)
+        for (int r = 0; r < 4; r++) t.m[c][r] = acc.r[r][c];
+    return t;
+}
+
 std::unique_ptr<LoadedMesh> LoadMeshAsset(const std::string& path) {
     std::ifstream in(path, std::ios::binary);
     if (!in) return nullptr;
@@ -391,16 +406,7 @@ std::unique_ptr<LoadedMesh> LoadMeshAsset(const std::string& path) {
     in.read(reinterpret_cast<char*>(mesh->normals.data()), (std::streamsize)nv * 12);
     in.read(reinterpret_cast<char*>(mesh->indices.data()), (std::streamsize)nf * 12);
     if (!in) return nullptr;
-    // aiMatrix4x4::RotationX(-(float)M_PI / 2) as the accumulated root transform, times the
-    // (identity) root and mesh node transforms, then convert_matrix (transpose into glm).
-    const float a = -3.14159265358979323846f / 2;
-    AiMat rx = ai_identity();
-    rx.r[1][1] = rx.r[2][2] = rth::hcos(a);
-    rx.r[2][1] = rth::hsin(a);
-    rx.r[1][2] = -rx.r[2][1];
-    AiMat acc = ai_mul(ai_mul(rx, ai_identity()), ai_identity());
-    for (int c = 0; c < 4; c++)
-        for (int r = 0; r < 4; r++) mesh->transform.m[c][r] = acc.r[r][c];
+    mesh->transform = ImporterRootTransform();
     return mesh;
 }
 
@@ -582,7 +588,9 @@ void rt_scene_add_sphere(rt_scene* s, const float p[3], float radius, int materi
     s->scene.AddSphere(v3(p), radius, material);
 }
 int rt_scene_add_mesh_file(rt_scene* s, const char* path, const float transform[16], int material) {
-    auto mesh = RayTracing::LoadMeshAsset(path);
+    const std::string p(path);
+    const bool obj = p.size() > 4 && (p.compare(p.size() - 4, 4, ".obj") == 0 || p.compare(p.size() - 4, 4, ".OBJ") == 0);
+    auto mesh = obj ? RayTracing::LoadObjMesh(p) : RayTracing::LoadMeshAsset(p);
     if (!mesh) return 1;
     rth::mat4 t;
     std::memcpy(t.m, transform, sizeof(t.m));

@@ -95,6 +95,10 @@ struct LoadedMesh {
     mat4 transform;                // node transform incl. the importer's root rotation
 };
 std::unique_ptr<LoadedMesh> LoadMeshAsset(const std::string& path);
+// Wavefront OBJ through the reference importer's post-processing, restated (objload.cpp).
+std::unique_ptr<LoadedMesh> LoadObjMesh(const std::string& path, float smoothing_angle_deg = 100.0f);
+// aiMatrix4x4::RotationX(-pi/2) at the root, as utils/AssimpLoader.cpp:47-48 applies it.
+mat4 ImporterRootTransform();
 
 // Scene.h:87-129
 struct Scene : public GPUScene {

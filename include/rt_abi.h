@@ -249,8 +249,9 @@ void rt_scene_add_triangle(rt_scene* scene, const float a[3], const float b[3], 
 void rt_scene_add_quad(rt_scene* scene, const float a[3], const float b[3], const float c[3], const float d[3],
                        int material);
 void rt_scene_add_sphere(rt_scene* scene, const float position[3], float radius, int material);
-/* Scene::AddLoadedScene with a mesh asset (assets/bunny_mesh.bin format) and a column-major
- * 4x4 transform.  Returns 0 or an error code. */
+/* Scene::AddLoadedScene with a mesh file -- a Wavefront .obj (imported like the reference's
+ * assimp post-processing, objload.cpp) or a mesh asset (assets/bunny_mesh.bin format) -- and a
+ * column-major 4x4 transform.  Returns 0 or an error code. */
 int rt_scene_add_mesh_file(rt_scene* scene, const char* path, const float transform[16], int material);
 /* Environment cube map from an asset (assets/sunset_cube128.bin) or a legacy fp32 DDS. */
 int rt_scene_set_environment_file(rt_scene* scene, const char* path);
