@@ -36,7 +36,7 @@ def main():
 
     stats = os.path.join(a.src, "prof_trace", "run_kernel_stats.csv")
     if a.kernel is None and os.path.exists(stats):
-        rows = [r for r in csv.DictReader(open(stats)) if short(r["Name"]).startswith("render_fast_kernel<")
+        rows = [r for r in csv.DictReader(open(stats)) if short(r["Name"]).startswith("render_fast_kernel")
                 and ", false," in short(r["Name"])]
         a.kernel = short(max(rows, key=lambda r: float(r["TotalDurationNs"]))["Name"]) if rows else None
     summary = {"config": a.config, "kernel": a.kernel}
