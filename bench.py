@@ -4,11 +4,17 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
 
 N = 1 runs BASELINE.json configs[1] (Stanford bunny scene, 1920x1080, 8 spp, 6 bounces).
-N > 1 (launched by torch.distributed.run, one process per GPU): the SAME frame is split into
-16x16 tiles dealt round-robin over the ranks (strong scaling); each rank renders its tiles
-into a compact shard, and one RCCL gather over xGMI assembles the frame on rank 0, where a
-kernel un-permutes it into the pitched surface.  Timing: barrier + synchronize on both sides
-of exactly K steps, max over ranks.
+N > 1 (launched by torch.distributed.run, one process per GPU): the frame is cut into 16x16
+tiles dealt round-robin over the ranks; each rank renders its tiles into a compact shard, and
+one RCCL gather over xGMI assembles the frame on rank 0, where a kernel un-permutes it into the
+pitched surface.  The gather of frame i runs on its own stream, overlapped with the render of
+frame i+1 (each rank keeps its own shard history, so the next frame does not wait for it).
+  --scaling weak (default): per-GPU work fixed -- the same camera at sqrt(N) x the resolution
+      per axis (N = 4: 3840x2160), so each rank renders about one 1920x1080 frame of tiles.
+  --scaling strong: the 1920x1080 frame itself split N ways.  Its speedup is capped by the
+      heaviest pixel: samples of a pixel share one RNG stream and run in order, and the
+      costliest pixel's 8 samples take ~11 ms alone ("Multi-GPU").
+Timing: barrier + synchronize on both sides of exactly K steps, max over ranks.
 
 Rank 0 prints one JSON line.  value = ray segments traced (GetRayHit calls, counted exactly by
 the kernel) per second over the whole job, in Mrays/s.  roofline = the render kernel's
@@ -71,6 +77,15 @@ def setup_dist(backend="nccl", same_device=False):
     return rank, world
 
 
+def weak_size(width, height, world):
+    """The weak-scaled frame for N ranks: sqrt(N) x the resolution per axis, width a multiple of
+    the 16-pixel tile, aspect kept (1920x1080: N=2 2720x1530, N=4 3840x2160, N=8 5424x3051)."""
+    if world <= 1:
+        return width, height
+    w = int(round(width * world ** 0.5 / 16.0)) * 16
+    return w, int(round(w * height / width))
+
+
 def cpu_baseline(cfg, sample_rows=None):
     """Oracle ("port") on this host's cores: bounded sample of the same frame (rows)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -107,7 +122,9 @@ def check_unsharded(rt, scene_name, W, H, spp, bounces, frames, final):
     for i in range(frames):
         rt.render(scene, bufs[i & 1], bufs[(i + 1) & 1], W, H, spp, bounces, i)
     torch.cuda.synchronize()
-    return bool(torch.equal(rt.surface_view(bufs[(frames - 1) & 1], W), rt.surface_view(final, W)))
+    # bitwise (same GPU, so NaNs from the reference arithmetic carry the same bits too)
+    a = rt.surface_view(bufs[(frames - 1) & 1], W).contiguous().view(torch.int32)
+    return bool(torch.equal(a, rt.surface_view(final, W).contiguous().view(torch.int32)))
 
 
 def load_traffic(cfg):
@@ -133,6 +150,8 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=0, help="rows of the frame the CPU baseline renders (0 = auto)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--same-device", action="store_true", help="every rank on GPU 0 (rehearsal on a one-GPU box)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="N > 1: weak = sqrt(N) x resolution per axis (per-GPU work fixed); strong = same frame")
     ap.add_argument("--check", action="store_true",
                     help="after timing, rank 0 re-renders the same frames unsharded and compares the final frame")
     args = ap.parse_args()
@@ -141,6 +160,9 @@ def main():
     assert world == args.gpus or world == 1, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     rt = G.load_package()
     scene_name, W, H, SPP, BOUNCES, desc = CONFIGS[args.config]
+    if world > 1 and args.scaling == "weak":
+        W, H = weak_size(W, H, world)
+        desc = f"{desc}, weak-scaled to {W}x{H} for {world} GPUs (same camera)"
     dev = torch.device("cuda", torch.cuda.current_device())
     stream = torch.cuda.current_stream()
 
@@ -186,8 +208,16 @@ def main():
     n_total = args.warmup + args.steps
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_total)]
 
+    # gather/render overlap (RCCL only; the gloo rehearsal stages through host memory in line)
+    comm = torch.cuda.Stream() if sharded and args.backend == "nccl" else None
+    rendered = torch.cuda.Event()
+    gathered_ev = [torch.cuda.Event(), torch.cuda.Event()]  # the gather that last read bufs[j]
+    gather_pending = [False, False]
+
     def step(i):
         cur, prev = bufs[i & 1], bufs[(i + 1) & 1]
+        if comm is not None and gather_pending[i & 1]:
+            stream.wait_event(gathered_ev[i & 1])  # frame i-2's gather still reads `cur`
         ev[i][0].record(stream)
         if sharded:
             rt.render(scene, None, prev, W, H, SPP, BOUNCES, i, rank, world, out_shard=cur,
@@ -196,7 +226,16 @@ def main():
             rt.render(scene, cur, prev, W, H, SPP, BOUNCES, i,
                       segment_counter=seg_counter if i >= args.warmup else None)
         ev[i][1].record(stream)
-        if sharded:
+        if comm is not None:
+            rendered.record(stream)
+            comm.wait_event(rendered)
+            with torch.cuda.stream(comm):
+                rt.sharding.gather_shards(cur, rank, world, out=gathered)
+                if rank == 0:
+                    rt.unshard(frame, W, H, world, gathered, per_shard)
+                gathered_ev[i & 1].record(comm)
+            gather_pending[i & 1] = True
+        elif sharded:
             rt.sharding.gather_shards(cur, rank, world, out=gathered)
             if rank == 0:
                 rt.unshard(frame, W, H, world, gathered, per_shard)
@@ -236,7 +275,8 @@ def main():
     final = (frame if sharded else bufs[(n_total - 1) & 1])
     if rank == 0:
         img = rt.surface_view(final, W)
-        finite = bool(torch.isfinite(img).all().item())
+        bad = (~torch.isfinite(img)).any(-1).nonzero()
+        finite = bad.shape[0] == 0
         result = {
             "metric": "Mrays/s + achieved HBM GB/s, Stanford bunny 1920x1080x8spp @1/2/4/8 GPU",
             "value": round(segs_total / elapsed / 1e6, 2),
@@ -246,7 +286,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.scaling if sharded else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (reference scene: Cornell box + Stanford bunny + HDR sky, seed 0xDEADBEEF)",
@@ -262,6 +302,8 @@ def main():
             "setup_s": round(setup_s, 2),
             "image_finite": finite,
         }
+        if not finite:  # (y, x) of non-finite pixels; the reference arithmetic can produce them too
+            result["nonfinite_pixels"] = bad[:8].tolist()
         if args.check:
             result["check_equal"] = check_unsharded(rt, scene_name, W, H, SPP, BOUNCES, n_total, final)
         if world == 1 and not args.no_cpu_baseline:

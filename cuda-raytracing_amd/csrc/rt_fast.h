@@ -738,6 +738,9 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
             if (STATS) {
                 c.w_small += (threadIdx.x & 63) == 0;
                 c.l_small += small;
+            } else if (TIMING) {
+                c.w_small++;
+                c.l_small += small;
             }
             if (small) active = small_step<STATS>(nodes4, tris, stk, R, h, T, c);
             continue;

@@ -504,6 +504,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
             }
         }
         if (!__ballot(path)) break;
+        if (MODE & 8) c.w_iter++;
         if (STATS) {
             c.w_seg += (threadIdx.x & 63) == 0;
             c.l_seg += path;
@@ -602,6 +603,12 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
         if ((threadIdx.x & 63) == 0) atomicAdd(a.seg_counter, v);
     }
+    unsigned long long lane_max = c.l_small;  // the busiest lane's small steps (timing frame)
+    if (MODE & 8)
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long o = __shfl_xor(lane_max, off);
+            lane_max = o > lane_max ? o : lane_max;
+        }
     if ((MODE & 8) && a.stats && threadIdx.x == 0) {  // timing frame: per-wave phase clocks
         atomicAdd(a.stats + RT_STAT_CYCLES_SMALL, c.cy_small);
         atomicAdd(a.stats + RT_STAT_CYCLES_BIG, c.cy_big);
@@ -609,6 +616,18 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
         atomicAdd(a.stats + RT_STAT_ROUNDS_COOP, c.r_coop);
         atomicAdd(a.stats + RT_STAT_ROUNDS_SHARED, c.r_shared);
         atomicAdd(a.stats + RT_STAT_COOP_RAYS, c.coop_rays);
+        // RT_TUNE bit 11: per-wave clocks (start, end) after the counters, for load-balance analysis
+        if (a.tune & 2048u) {
+            unsigned long long* w = a.stats + RT_STAT_COUNT + 8 * (size_t)blockIdx.x;
+            w[0] = t_start;
+            w[1] = __builtin_amdgcn_s_memtime();
+            w[2] = c.cy_small;
+            w[3] = c.cy_big;
+            w[4] = c.r_coop + c.r_shared;
+            w[5] = c.w_iter;
+            w[6] = c.w_small;
+            w[7] = lane_max;
+        }
     }
     if (STATS) {
         atomicAdd(a.stats + RT_STAT_SEGMENTS, c.seg);
@@ -748,6 +767,7 @@ hipError_t launch_fast_m(const RenderArgs& args, int tiles, hipStream_t stream) 
 
 template <int STACK, bool STATS>
 hipError_t launch_fast_t(const RenderArgs& args, int tiles, hipStream_t stream) {
+
     // statistics: the reference's work on scalar records (RT_TUNE bit 7: through the leaf trees);
     // RT_TUNE bit 8: a timing frame of the production kernel instead (phase clocks, no counts)
     if (STATS && (args.tune & 256u)) return launch_fast_m<STACK, false, 9>(args, tiles, stream);
@@ -892,6 +912,8 @@ static int foreign_mirror(const GPUScene* scene, hipStream_t st, MirrorDevice* o
     return 0;
 }
 
+// Per-configuration wave-cost history for the priority scheme in render_fast_body: one uint32
+// per workgroup and three rotating uint64 sums, kept per (device, frame size, shard).
 extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void* stream) {
     if (!p || !scene) return set_error("rt_render: null argument");
     if (p->width <= 0 || p->height <= 0 || p->spp <= 0 || p->bounces < 0)

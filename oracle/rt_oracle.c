@@ -820,9 +820,9 @@ static v3 ray_color(const OScene* s, v3 ro, v3 rd, ORng* rng, int bounces, float
  * seeded with curand_init(seed, y*width + x, 0).  last: float4 history in out's layout, or
  * NULL (zeros).  threads <= 0: OpenMP default.  stats: OStats (8 uint64) or NULL.
  */
-int oracle_render(const OScene* s, int width, int height, int spp, int bounces, int frame_index, uint32_t seed,
-                  uint32_t* rng, const float* last, float* out, int row_begin, int row_end, int threads,
-                  uint64_t* stats) {
+static int render_rows(const OScene* s, int width, int height, int spp, int bounces, int frame_index, uint32_t seed,
+                       uint32_t* rng, const float* last, float* out, int row_begin, int row_end, int threads,
+                       uint64_t* stats, uint32_t* costs) {
     if (!s || width <= 0 || height <= 0 || row_begin < 0 || row_end > height || row_begin > row_end) return 1;
     OCamera cam;
     o_camera(s, width, height, &cam);
@@ -846,6 +846,7 @@ int oracle_render(const OScene* s, int width, int height, int spp, int bounces, 
             if (rng) { r.d = rng[6 * pid]; memcpy(r.v, rng + 6 * pid + 1, 20); }
             else rng_init(seed, pid, &r);
             float acc[4] = {0, 0, 0, 0};
+            const OStats st0 = st;
             for (int smp = 0; smp < spp; smp++) {
                 float ru = rng_uniform(&r), rv = rng_uniform(&r);
                 float ux = ((float)x + ru) / (float)width, uy = ((float)y + rv) / (float)height;
@@ -862,6 +863,10 @@ int oracle_render(const OScene* s, int width, int height, int spp, int bounces, 
             }
             out[o + 3] = 1.0f;
             if (rng) { rng[6 * pid] = r.d; memcpy(rng + 6 * pid + 1, r.v, 20); }
+            if (costs) {
+                uint32_t* c = costs + 3 * ((size_t)(y - row_begin) * width + x);
+                c[0] = (uint32_t)(st.seg - st0.seg), c[1] = (uint32_t)(st.nodes - st0.nodes), c[2] = (uint32_t)(st.tris - st0.tris);
+            }
         }
 #ifdef _OPENMP
 #pragma omp critical(oracle_stats)
@@ -873,4 +878,17 @@ int oracle_render(const OScene* s, int width, int height, int spp, int bounces, 
     }
     if (stats) memcpy(stats, &total, sizeof total);
     return 0;
+}
+int oracle_render(const OScene* s, int width, int height, int spp, int bounces, int frame_index, uint32_t seed,
+                  uint32_t* rng, const float* last, float* out, int row_begin, int row_end, int threads,
+                  uint64_t* stats) {
+    return render_rows(s, width, height, spp, bounces, frame_index, seed, rng, last, out, row_begin, row_end, threads,
+                       stats, NULL);
+}
+/* oracle_render plus per-pixel work: costs[3 * pixel] = (segments, node visits, triangle tests) */
+int oracle_render_costs(const OScene* s, int width, int height, int spp, int bounces, int frame_index, uint32_t seed,
+                        uint32_t* rng, const float* last, float* out, int row_begin, int row_end, int threads,
+                        uint64_t* stats, uint32_t* costs) {
+    return render_rows(s, width, height, spp, bounces, frame_index, seed, rng, last, out, row_begin, row_end, threads,
+                       stats, costs);
 }

@@ -86,3 +86,15 @@ def test_tile_deal_balanced_and_complete():
     per = max(sh.tiles_of_shard(40, 24, r, n) for r in range(n))
     pix = list(chain.from_iterable(zip(*[a[a >= 0] for a in sh.slot_pixels(40, 24, r, n, per)]) for r in range(n)))
     assert len(pix) == 40 * 24 == len(set(pix))
+
+
+def test_weak_scaling_frame_sizes():
+    """bench.py --scaling weak: sqrt(N) x resolution per axis, tile-aligned width, 16:9 kept."""
+    import bench
+
+    assert bench.weak_size(1920, 1080, 1) == (1920, 1080)
+    assert bench.weak_size(1920, 1080, 4) == (3840, 2160)
+    for n in (2, 4, 8):
+        w, h = bench.weak_size(1920, 1080, n)
+        assert w % 16 == 0 and abs(w / h - 16 / 9) < 2e-3
+        assert abs(w * h / (1920 * 1080 * n) - 1.0) < 0.01

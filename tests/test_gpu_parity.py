@@ -256,3 +256,36 @@ def test_foreign_gpuscene(rt):
     finally:
         for p in owned.values():
             rt.lib().rt_free(p)
+
+
+def test_nan_pixel_tile(rt):
+    """A pixel whose reference arithmetic yields NaN: (1062, 756) of the 2720x1530 frame (the
+    2-GPU weak-scaled bench frame) goes NaN in frame 0, in the oracle as on the GPU.  Only its
+    16x16 tile is rendered (a one-tile shard: shard_count = tiles, shard_index = that tile),
+    two progressive frames: the same values bit for bit and NaN in the same places (a NaN's
+    payload bits are the ISA's choice: x86 and the GPU differ, as the reference's would)."""
+    w, h, spp, bounces, px, py = 2720, 1530, 8, 6, 1062, 756
+    tiles_x = (w + 15) // 16
+    n = tiles_x * ((h + 15) // 16)
+    tile = (py // 16) * tiles_x + px // 16
+    s = make_scene(rt, "bunny", w, h)
+    rng = rt.alloc_rng(256)
+    rt.init_rng_states(rng, w, h, T.SEED, tile, n)
+    s.upload(rng.data_ptr())
+    bufs = [torch.zeros((256, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
+    o = T.OracleScene("bunny")
+    orng = T.oracle_rng_frame(T.SEED, w, h)
+    last = None
+    y0, x0 = (py // 16) * 16, (px // 16) * 16
+    xs, ys = rt.sharding.slot_pixels(w, h, tile, n)
+    for f in range(2):
+        rt.render(s, None, bufs[(f + 1) & 1], w, h, spp, bounces, f, tile, n, out_shard=bufs[f & 1])
+        torch.cuda.synchronize()
+        got = bufs[f & 1].cpu().numpy()
+        img = o.render(w, h, spp, bounces, frame_index=f, rng=orng, last=last, rows=(y0, y0 + 16))
+        last = img
+        want = img[ys - y0, xs]
+        assert not np.isfinite(want[(ys == py) & (xs == px)]).all(), "expected the reference NaN pixel"
+        nan_g, nan_w = np.isnan(got), np.isnan(want)
+        assert np.array_equal(nan_g, nan_w), f"frame {f}: NaN positions differ"
+        assert np.array_equal(got[~nan_g].view(np.uint32), want[~nan_w].view(np.uint32)), f"frame {f}: tile differs"
