@@ -17,7 +17,8 @@ the native library is missing or fails to load this module raises.
 import ctypes
 import os
 
-import torch  # imported first so librt_hip.so binds to the HIP runtime torch already loaded
+import numpy as np
+import torch  # imported before the library so librt_hip.so binds to the HIP runtime torch already loaded
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT_DIR = os.path.dirname(PKG_DIR)
@@ -78,6 +79,9 @@ SIGNATURES = {
     "rt_init_rng": (_I, [_P, _I, _I, _I, _I, _U32, _P]),
     "rt_shard_tiles": (ctypes.c_int64, [_I, _I, _I, _I]),
     "rt_unshard": (_I, [_P, _U64, _I, _I, _I, _P, ctypes.c_int64, _P]),
+    "rt_tonemap_srgb8": (_I, [_P, _U64, _I, _I, _P, _P]),
+    "rt_write_pfm": (_I, [ctypes.c_char_p, _P, _U64, _I, _I]),
+    "rt_write_ppm": (_I, [ctypes.c_char_p, _P, _I, _I]),
     "rt_set_device": (_I, [_I]),
     "rt_malloc": (_I, [ctypes.POINTER(_P), _SZ]),
     "rt_malloc_pitch": (_I, [ctypes.POINTER(_P), ctypes.POINTER(_SZ), _SZ, _SZ]),
@@ -317,6 +321,28 @@ def unshard(surface, width, height, shard_count, shards, per_shard, stream=None)
                             ctypes.c_void_p(shards.data_ptr()), per_shard, _stream_ptr(stream)), "rt_unshard")
 
 
+def tonemap(surface, width, height, stream=None):
+    """The reference viewer's display transform (main.cpp:78-94 into an sRGB back buffer):
+    [H, W, 3] uint8 on the GPU, rows top to bottom."""
+    out = torch.empty((height, width, 3), dtype=torch.uint8, device=surface.device)
+    _check(lib().rt_tonemap_srgb8(ctypes.c_void_p(surface.data_ptr()), surface.shape[1] * 4, width, height,
+                                  ctypes.c_void_p(out.data_ptr()), _stream_ptr(stream)), "rt_tonemap_srgb8")
+    return out
+
+
+def write_pfm(path, surface, width, height):
+    """Linear RGB of a pitched float4 surface (torch, any device; or a numpy [H, row] array) as
+    PFM, rows bottom to top -- the surface's own order."""
+    host = surface.detach().to("cpu").contiguous().numpy() if isinstance(surface, torch.Tensor) else np.ascontiguousarray(surface, dtype=np.float32)
+    _check(lib().rt_write_pfm(os.fsencode(path), host.ctypes.data, host.shape[1] * 4, width, height), "rt_write_pfm")
+
+
+def write_ppm(path, rgb):
+    """[H, W, 3] uint8 (tonemap's output, any device) as binary PPM."""
+    host = rgb.detach().to("cpu").contiguous().numpy() if isinstance(rgb, torch.Tensor) else np.ascontiguousarray(rgb, dtype=np.uint8)
+    _check(lib().rt_write_ppm(os.fsencode(path), host.ctypes.data, host.shape[1], host.shape[0]), "rt_write_ppm")
+
+
 def raytracing_process(surface, last, width, height, frame_index, scene):
     """The reference entry point (main_raytracing.cu:202): spp 5, 6 bounces, null stream."""
     lib().raytracing_process(ctypes.c_void_p(surface.data_ptr()), ctypes.c_void_p(last.data_ptr()), width, height,
@@ -363,6 +389,16 @@ class RayTracer:
         self.last_frame.copy_(self.surface)
         self.frame_index += 1
         return surface_view(self.surface, self.width)
+
+    def save(self, path):
+        """The current frame: ``.pfm`` linear RGB, ``.ppm`` as the reference's viewer shows it
+        (exposure 0.5, ACES film, sRGB; main.cpp:78-94, 438)."""
+        if str(path).lower().endswith(".pfm"):
+            write_pfm(path, self.surface, self.width, self.height)
+        elif str(path).lower().endswith(".ppm"):
+            write_ppm(path, tonemap(self.surface, self.width, self.height))
+        else:
+            raise ValueError("RayTracer.save: .pfm or .ppm")
 
 
 from . import sharding  # noqa: E402  (multi-GPU tile bookkeeping; the data path is in librt_hip.so)

@@ -27,8 +27,8 @@ ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 # Numerics flags shared by every translation unit of the product: no FMA contraction, IEEE
 # fp32 division and square root (bit-exact agreement between host code, kernels and oracle).
 FP_FLAGS = ["-ffp-contract=off", "-fno-fast-math"]
-HOST_SOURCES = ["scene.cpp", "objload.cpp", "mirror.cpp", "leaftree.cpp", "xorwow.cpp"]
-HIP_SOURCES = ["rt_kernel.hip"]
+HOST_SOURCES = ["scene.cpp", "objload.cpp", "mirror.cpp", "leaftree.cpp", "xorwow.cpp", "image.cpp"]
+HIP_SOURCES = ["rt_kernel.hip", "image.hip"]
 
 
 def _run(cmd):

@@ -218,6 +218,18 @@ int rt_unshard(void* surface, uint64_t pitch, int width, int height, int shard_c
                int64_t tiles_per_shard_max, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Frame output (the viewer path: main.cpp:66-94 draws the surface with exposure 0.5 + ACES film
+ * into an sRGB back buffer, main.cpp:438).  For looking at frames; not on the render path.
+ * ------------------------------------------------------------------------------------- */
+/* Tonemap a pitched float4 surface into width*height*3 bytes of DEVICE memory, rows top to
+ * bottom (display order): sRGB8(ACESFilm(0.5 * rgb)), IEC sRGB encode.  Returns 0 or nonzero. */
+int rt_tonemap_srgb8(const void* surface, uint64_t pitch, int width, int height, uint8_t* out_rgb, void* stream);
+/* Host files: PFM of a HOST copy of the surface (linear RGB, rows bottom to top as PFM
+ * stores them = the surface's row order), and binary PPM of top-to-bottom RGB8 rows. */
+int rt_write_pfm(const char* path, const float* rgba, uint64_t pitch, int width, int height);
+int rt_write_ppm(const char* path, const uint8_t* rgb, int width, int height);
+
+/* ---------------------------------------------------------------------------------------
  * Device memory / texture shim (replaces utils/CUDAHelper.h and utils/CUDATexture.*).
  * ------------------------------------------------------------------------------------- */
 int rt_set_device(int device);
