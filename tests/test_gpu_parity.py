@@ -289,3 +289,42 @@ def test_nan_pixel_tile(rt):
         nan_g, nan_w = np.isnan(got), np.isnan(want)
         assert np.array_equal(nan_g, nan_w), f"frame {f}: NaN positions differ"
         assert np.array_equal(got[~nan_g].view(np.uint32), want[~nan_w].view(np.uint32)), f"frame {f}: tile differs"
+
+
+def _tile_shard(rt, scene, w, h, spp, bounces, px, py, frame_index=0, last=None):
+    """Render only the 16x16 tile holding pixel (px, py) of a w x h frame: a one-tile shard
+    (shard_count = tiles, shard_index = that tile), fresh RNG.  Returns (slots float4 [256],
+    slot x, slot y)."""
+    tiles_x = (w + 15) // 16
+    n = tiles_x * ((h + 15) // 16)
+    tile = (py // 16) * tiles_x + px // 16
+    rng = rt.alloc_rng(256)
+    rt.init_rng_states(rng, w, h, T.SEED, tile, n)
+    scene.upload(rng.data_ptr())
+    out = torch.zeros((256, 4), dtype=torch.float32, device="cuda")
+    rt.render(scene, None, last, w, h, spp, bounces, frame_index, tile, n, out_shard=out)
+    torch.cuda.synchronize()
+    xs, ys = rt.sharding.slot_pixels(w, h, tile, n)
+    return out.cpu().numpy(), xs, ys
+
+
+@pytest.mark.parametrize("cfg,which,w,h,spp,picks", [
+    # BASELINE configs[2]: 4K, 64 spp -- tiles on the bunny, in the box (spheres), on the floor
+    ("config3", "bunny", 3840, 2160, 64, [(900, 1400), (1920, 1300), (2600, 1950)]),
+    # configs[3]: the 4-bunny scene (leaf trees in the production kernel)
+    ("config4", "bunny4", 1920, 1080, 8, [(200, 700), (520, 860), (960, 540)]),
+    # configs[4]: the 1M-triangle plane (708 x 708 quads)
+    ("config5", "plane1m", 1920, 1080, 1, [(7, 3), (960, 540), (1900, 1070)]),
+])
+def test_full_size_tiles(rt, cfg, which, w, h, spp, picks):
+    """Full-size BASELINE configurations, tiles rendered alone through the shard path and
+    compared bit for bit with the oracle's rendering of the rows that hold them."""
+    s = make_scene(rt, which, w, h)
+    o = T.OracleScene(which)
+    for px, py in picks:
+        got, xs, ys = _tile_shard(rt, s, w, h, spp, 6, px, py)
+        y0 = (py // 16) * 16
+        rows = min(16, h - y0)
+        want = o.render(w, h, spp, 6, rows=(y0, y0 + rows))
+        ok = xs >= 0
+        assert_close(got[ok], want[ys[ok] - y0, xs[ok]], f"{cfg} tile at ({px}, {py})")
