@@ -22,6 +22,14 @@ void put_flat(float* o, const float* p0, const float* p1, const float* p2, uint3
     std::memcpy(&o[9], &face, 4);
     o[10] = o[11] = 0.0f;
 }
+// Two FlatTri records a, b (b null: an all-zero triangle, never accepted) as one pair record.
+void put_pair(float* q, const float* a, const float* b) {
+    static const float zero[12] = {};
+    if (!b) b = zero;
+    for (int c = 0; c < 9; c++) q[2 * c] = a[c], q[2 * c + 1] = b[c];
+    std::memcpy(&q[18], &a[9], 4);
+    std::memcpy(&q[19], &b[9], 4);
+}
 }  // namespace
 
 void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t* fi, size_t index_count,
@@ -44,6 +52,7 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
     out->depth = 0;
     out->fast = true;
     std::vector<uint32_t> big;
+    out->spairs.assign(index_count * 20, 0.0f);
     if (node_count == 0) return;
     std::vector<std::pair<uint32_t, int>> st{{0u, 0}};
     size_t visited = 0;
@@ -61,7 +70,12 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
         if (nd.prim_count > 0) {
             if ((size_t)nd.first_index + nd.prim_count > index_count) bad("leaf range out of range");
             out->depth = std::max(out->depth, d);
-            if (nd.prim_count > MIRROR_BIG_LEAF) big.push_back(n);
+            if (nd.prim_count > MIRROR_BIG_LEAF)
+                big.push_back(n);
+            else
+                for (uint32_t j = 0; j < nd.prim_count; j += 2)
+                    put_pair(&out->spairs[((size_t)nd.first_index + j) * 20], &out->tris[((size_t)nd.first_index + j) * 12],
+                             j + 1 < nd.prim_count ? &out->tris[((size_t)nd.first_index + j + 1) * 12] : nullptr);
         } else {
             st.push_back({nd.first_index, d + 1});
             st.push_back({nd.first_index + 1, d + 1});
@@ -94,16 +108,9 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
         std::memcpy(&lead[10], &po, 4);
         std::memcpy(&lead[11], &pf, 4);
         for (uint32_t j = 0; j < nd.prim_count; j += 2) {
-            const float* a = &out->tris[((size_t)nd.first_index + j) * 12];
-            static const float zero[12] = {};
-            const float* b = j + 1 < nd.prim_count ? &out->tris[((size_t)nd.first_index + j + 1) * 12] : zero;
             float q[20];
-            for (int c = 0; c < 9; c++) q[2 * c] = a[c], q[2 * c + 1] = b[c];
-            uint32_t fa, fb = 0;
-            std::memcpy(&fa, &a[9], 4);
-            if (b != zero) std::memcpy(&fb, &b[9], 4);
-            std::memcpy(&q[18], &fa, 4);
-            std::memcpy(&q[19], &fb, 4);
+            put_pair(q, &out->tris[((size_t)nd.first_index + j) * 12],
+                     j + 1 < nd.prim_count ? &out->tris[((size_t)nd.first_index + j + 1) * 12] : nullptr);
             out->pairs.insert(out->pairs.end(), q, q + 20);
         }
     }
@@ -130,13 +137,15 @@ void release(Entry& e) {
 }  // namespace
 
 int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owned, uint64_t fingerprint) {
-    const size_t nt = m.tris.size() * 4, np = m.pairs.size() * 4, nk = m.tree.size() * 4, nl = m.ltris.size() * 4;
+    const size_t nt = m.tris.size() * 4, np = m.pairs.size() * 4, nk = m.tree.size() * 4, nl = m.ltris.size() * 4,
+                 ns = m.spairs.size() * 4;
     void* block = nullptr;
-    if (rt_malloc(&block, nt + np + nk + nl + 64) != 0) return -1;
+    if (rt_malloc(&block, nt + np + nk + nl + ns + 64) != 0) return -1;
     char* b = static_cast<char*>(block);
     if ((nt && rt_memcpy_h2d(b, m.tris.data(), nt) != 0) || (np && rt_memcpy_h2d(b + nt, m.pairs.data(), np) != 0) ||
         (nk && rt_memcpy_h2d(b + nt + np, m.tree.data(), nk) != 0) ||
-        (nl && rt_memcpy_h2d(b + nt + np + nk, m.ltris.data(), nl) != 0)) {
+        (nl && rt_memcpy_h2d(b + nt + np + nk, m.ltris.data(), nl) != 0) ||
+        (ns && rt_memcpy_h2d(b + nt + np + nk + nl, m.spairs.data(), ns) != 0)) {
         rt_free(block);
         return -1;
     }
@@ -145,6 +154,7 @@ int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owne
     e.dev.pairs = np ? b + nt : nullptr;
     e.dev.tree = nk ? b + nt + np : nullptr;
     e.dev.ltris = nl ? b + nt + np + nk : nullptr;
+    e.dev.spairs = ns ? b + nt + np + nk + nl : nullptr;
     e.dev.depth = m.depth;
     e.dev.fast = m.fast;
     e.dev.owned = owned;

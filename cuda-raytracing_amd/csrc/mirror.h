@@ -12,6 +12,10 @@
 //           (v0z, e1x), (e1y, e1z), (e2x, e2y), (e2z_a, e2z_b, face_a, face_b) -- the operand
 //           layout of packed fp32 instructions; an odd leaf ends with an all-zero triangle.  The
 //           leaf's first tris record holds po = its first pair, pf = 1 (0 for other leaves);
+//  * spairs for every leaf of at most BIG triangles, its triangles two by two in the pairs layout,
+//           the pair of triangles (i, i + 1) stored at record i (i = first, first + 2, ...; an
+//           odd leaf ends with an all-zero triangle), so a small leaf needs no index of its own;
+//           records at other positions are unused;
 //  * tree / ltris  for leaves of at least MIRROR_TREE_LEAF triangles, a leaf tree instead
 //           (leaftree.h): the first record holds po = the root node, pf = 2;
 //  * depth  the deepest leaf (sizes the traversal stack) and whether every node bound lies in
@@ -30,6 +34,7 @@ constexpr uint32_t MIRROR_TREE_LEAF = 1024;  // ... and leaves this large a leaf
 struct MirrorHost {
     std::vector<float> tris;      // 12 floats per record
     std::vector<float> pairs;     // 20 floats per pair
+    std::vector<float> spairs;    // 20 floats per triangle position (small leaves' pairs)
     std::vector<float> tree;      // 16 floats per leaf-tree node
     std::vector<float> ltris;     // 12 floats per leaf-tree triangle record
     int depth = 0;                // deepest leaf (root = 0) reachable from node 0
@@ -47,6 +52,7 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
 struct MirrorDevice {
     const void* tris = nullptr;
     const void* pairs = nullptr;
+    const void* spairs = nullptr;
     const void* tree = nullptr;
     const void* ltris = nullptr;
     int depth = -1;

@@ -46,8 +46,9 @@ struct RenderArgs {
     const float4* pairs;  // big leaves' triangles in packed pairs (mirror.h) or null
     const float4* tree;   // leaf trees of huge leaves (leaftree.h) or null
     const float4* ltris;  // their triangle records
+    const float4* spairs; // small leaves' triangles in packed pairs, pair (i, i+1) at record i, or null
     uint32_t tune;  // A/B knobs (RT_TUNE, rt_render): bit0 no cooperative leaf rounds, bit1 no pair
-                    // records, bit2 no leaf trees, bits 4-5 big-leaf mode (rt_kernel.hip launch_fast_t)
+                    // records, bit2 no leaf trees, bit3 no small-leaf pairs, bits 4-5 big-leaf mode (rt_kernel.hip launch_fast_t)
 };
 
 struct Counters {

@@ -627,11 +627,16 @@ __device__ __forceinline__ bool trav_begin(const float4* nodes4, const Ray& R, c
 // (Testing a small leaf in the same step as the inner node that entered it was measured slower:
 // 22.2 vs 20.6 ms, the extra divergence costs more than the saved iterations.)
 template <bool STATS, class C>
-__device__ __forceinline__ bool small_step(const float4* nodes4, const float4* tris, uint32_t* stk, const Ray& R,
-                                           Hit& h, Trav& T, C& c) {
+__device__ __forceinline__ bool small_step(const float4* nodes4, const float4* tris, const float4* spairs, uint32_t* stk,
+                                           const Ray& R, Hit& h, Trav& T, C& c) {
     if (T.count > 0) {
-        for (uint32_t i = T.first; i < T.first + T.count; i++)
-            test_triangle<STATS>(R, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], h, c);
+        if (!STATS && spairs) {
+            // two triangles per packed pair record (mirror.h spairs), in leaf order
+            for (uint32_t i = T.first; i < T.first + T.count; i += 2) pair_test(R, ld_pair(spairs, i), h);
+        } else {
+            for (uint32_t i = T.first; i < T.first + T.count; i++)
+                test_triangle<STATS>(R, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], h, c);
+        }
         return pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
     }
     if (inner_step<STATS>(nodes4, stk, T.sp, R, h.best, T.first, T.count, c)) return true;
@@ -726,7 +731,8 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
 // reference's triangle tests plus the tree's own work).
 template <bool STATS, int MODE, class C>
 __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, const float4* pairs,
-                                      const float4* tree, const float4* ltris, uint32_t tune, uint32_t* stk,
+                                      const float4* tree, const float4* ltris, const float4* spairs, uint32_t tune,
+                                      uint32_t* stk,
                                       const Ray& R, Hit& h, bool live, C& c) {
     Trav T{0, 0, 0};
     bool active = live && trav_begin<STATS>(nodes4, R, h, T, c);
@@ -742,7 +748,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                 c.w_small++;
                 c.l_small += small;
             }
-            if (small) active = small_step<STATS>(nodes4, tris, stk, R, h, T, c);
+            if (small) active = small_step<STATS>(nodes4, tris, spairs, stk, R, h, T, c);
             continue;
         }
         if (TIMING) {

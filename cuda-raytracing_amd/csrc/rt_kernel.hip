@@ -423,6 +423,71 @@ __global__ __launch_bounds__(WAVE) void render_kernel(RenderArgs a) {
     }
 }
 
+// ray_color's per-segment tail (main_raytracing.cu:118-158) for the segment whose closest hit is
+// `h`: emission, throughput, the next direction from 4 draws, Russian roulette; or the sky on a
+// miss.  Updates the path (ro, rd, color, thr); returns true when the path ends here.
+template <bool STATS>
+__device__ __forceinline__ bool shade_segment(const RenderArgs& a, const rtfast::Hit& h, rtm::f3& ro, rtm::f3& rd,
+                                              const rtm::f3 nd, rtm::Xorwow& rng, rtm::f3& color, rtm::f3& thr,
+                                              Counters& c) {
+    bool end = false;
+    if (h.kind != 0) {
+        if (STATS) c.hit++;
+        const rtm::f3 pos = rtm::add(ro, rtm::muls(nd, h.best));
+        rtm::f3 nrm;
+        uint32_t mat;
+        if (h.kind == 1) {
+            const GeometrySphere& sp = a.spheres[h.id];
+            nrm = rtm::divs(rtm::sub(pos, ld3(sp.position)), sp.radius);
+            mat = (uint32_t)sp.material;
+        } else {
+            const GPUFace f = a.faces[h.id];
+            const float bz = (1.0f - h.bx) - h.by;
+            nrm = rtm::normalize(rtm::add(rtm::add(rtm::muls(ld3(a.vertices[f.v0].normal), h.bx),
+                                                   rtm::muls(ld3(a.vertices[f.v1].normal), h.by)),
+                                          rtm::muls(ld3(a.vertices[f.v2].normal), bz)));
+            if (rtm::dot(nd, nrm) >= 0.0f) nrm = rtm::neg(nrm);
+            mat = f.material;
+        }
+        const GPUMaterial& m = a.materials[mat];
+        const float do_spec = (rng.uniform() < m.specular_percent) ? 1.0f : 0.0f;
+        color = rtm::add(color, rtm::mul(thr, ld3(m.emissive)));
+        const float om = 1.0f - do_spec;
+        thr = rtm::mul(thr, rtm::mk(m.albedo[0] * om + m.specular[0] * do_spec,
+                                    m.albedo[1] * om + m.specular[1] * do_spec,
+                                    m.albedo[2] * om + m.specular[2] * do_spec));
+        // GetRandomPointOnSphere (Random.h:23-46)
+        const float zz = rng.uniform() * 2.0f - 1.0f;
+        const float ang = rng.uniform() * 3.141592654f * 2.0f;
+        const float rr = sqrtf(1.0f - zz * zz);
+        const rtm::f3 sph = rtm::mk(rr * rtm::rt_cosf(ang), rr * rtm::rt_sinf(ang), zz);
+        const rtm::f3 diffuse = rtm::normalize(rtm::add(nrm, sph));
+        rtm::f3 spec = rtm::normalize(rtm::reflect(rd, nrm));
+        spec = rtm::normalize(rtm::mix(spec, diffuse, m.roughness * m.roughness));
+        const rtm::f3 ndir = rtm::normalize(rtm::add(rtm::muls(diffuse, om), rtm::muls(spec, do_spec)));
+        ro = rtm::add(pos, rtm::muls(nrm, 0.01f));
+        rd = ndir;
+        // Russian roulette (main_raytracing.cu:140-148)
+        const float p = rtm::gmax(thr.x, rtm::gmax(thr.y, thr.z));
+        if (rng.uniform() > p) {
+            end = true;
+        } else {
+            thr = rtm::muls(thr, 1.0f / p);
+        }
+    } else {
+        if (STATS) c.miss++;
+        if (a.sky) {
+            const rtm::f3 dir = rtd::quat_rotate(a.qw, a.qx, a.qy, a.qz, rd);
+            const rtm::f3 cs = rtd::cube_sample(a.sky, a.sky_n, dir);
+            const rtm::f3 cl = rtm::mk(rtm::gmin(rtm::gmax(cs.x, 0.0f), 50.0f), rtm::gmin(rtm::gmax(cs.y, 0.0f), 50.0f),
+                                       rtm::gmin(rtm::gmax(cs.z, 0.0f), 50.0f));
+            color = rtm::add(color, rtm::mul(thr, cl));
+        }
+        end = true;
+    }
+    return end;
+}
+
 // The production kernel: rt_fast.h traversal + a flat per-lane segment loop.
 // raytracing_kernel_main / ray_color (main_raytracing.cu:111-200) nest `for sample { for
 // bounce { ... break } }`; on a SIMD machine that makes every lane wait at the end of each
@@ -529,64 +594,10 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
             }
         }
         const rtfast::Ray R = rtfast::make_ray(ro, rd, nd, scene_fast);
-        rtfast::trace<STATS, MODE>(nodes4, tris, a.pairs, a.tree, a.ltris, a.tune, stk, R, h, path, c);
+        rtfast::trace<STATS, MODE>(nodes4, tris, a.pairs, a.tree, a.ltris, a.spairs, a.tune, stk, R, h, path, c);
         if (!path) continue;
 
-        bool end = false;
-        if (h.kind != 0) {
-            if (STATS) c.hit++;
-            const rtm::f3 pos = rtm::add(ro, rtm::muls(nd, h.best));
-            rtm::f3 nrm;
-            uint32_t mat;
-            if (h.kind == 1) {
-                const GeometrySphere& sp = a.spheres[h.id];
-                nrm = rtm::divs(rtm::sub(pos, ld3(sp.position)), sp.radius);
-                mat = (uint32_t)sp.material;
-            } else {
-                const GPUFace f = a.faces[h.id];
-                const float bz = (1.0f - h.bx) - h.by;
-                nrm = rtm::normalize(rtm::add(rtm::add(rtm::muls(ld3(a.vertices[f.v0].normal), h.bx),
-                                                       rtm::muls(ld3(a.vertices[f.v1].normal), h.by)),
-                                              rtm::muls(ld3(a.vertices[f.v2].normal), bz)));
-                if (rtm::dot(nd, nrm) >= 0.0f) nrm = rtm::neg(nrm);
-                mat = f.material;
-            }
-            const GPUMaterial& m = a.materials[mat];
-            const float do_spec = (rng.uniform() < m.specular_percent) ? 1.0f : 0.0f;
-            color = rtm::add(color, rtm::mul(thr, ld3(m.emissive)));
-            const float om = 1.0f - do_spec;
-            thr = rtm::mul(thr, rtm::mk(m.albedo[0] * om + m.specular[0] * do_spec,
-                                        m.albedo[1] * om + m.specular[1] * do_spec,
-                                        m.albedo[2] * om + m.specular[2] * do_spec));
-            // GetRandomPointOnSphere (Random.h:23-46)
-            const float zz = rng.uniform() * 2.0f - 1.0f;
-            const float ang = rng.uniform() * 3.141592654f * 2.0f;
-            const float rr = sqrtf(1.0f - zz * zz);
-            const rtm::f3 sph = rtm::mk(rr * rtm::rt_cosf(ang), rr * rtm::rt_sinf(ang), zz);
-            const rtm::f3 diffuse = rtm::normalize(rtm::add(nrm, sph));
-            rtm::f3 spec = rtm::normalize(rtm::reflect(rd, nrm));
-            spec = rtm::normalize(rtm::mix(spec, diffuse, m.roughness * m.roughness));
-            const rtm::f3 ndir = rtm::normalize(rtm::add(rtm::muls(diffuse, om), rtm::muls(spec, do_spec)));
-            ro = rtm::add(pos, rtm::muls(nrm, 0.01f));
-            rd = ndir;
-            // Russian roulette (main_raytracing.cu:140-148)
-            const float p = rtm::gmax(thr.x, rtm::gmax(thr.y, thr.z));
-            if (rng.uniform() > p) {
-                end = true;
-            } else {
-                thr = rtm::muls(thr, 1.0f / p);
-            }
-        } else {
-            if (STATS) c.miss++;
-            if (a.sky) {
-                const rtm::f3 dir = rtd::quat_rotate(a.qw, a.qx, a.qy, a.qz, rd);
-                const rtm::f3 cs = rtd::cube_sample(a.sky, a.sky_n, dir);
-                const rtm::f3 cl = rtm::mk(rtm::gmin(rtm::gmax(cs.x, 0.0f), 50.0f), rtm::gmin(rtm::gmax(cs.y, 0.0f), 50.0f),
-                                           rtm::gmin(rtm::gmax(cs.z, 0.0f), 50.0f));
-                color = rtm::add(color, rtm::mul(thr, cl));
-            }
-            end = true;
-        }
+        bool end = shade_segment<STATS>(a, h, ro, rd, nd, rng, color, thr, c);
         if (++bounce >= a.bounces) end = true;
         if (end) {
             acc_r += color.x;
@@ -972,6 +983,7 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     a.pairs = (a.tune & 2u) ? nullptr : (const float4*)mir.pairs;
     a.tree = (a.tune & 4u) ? nullptr : (const float4*)mir.tree;
     a.ltris = (const float4*)mir.ltris;
+    a.spairs = (a.tune & 8u) ? nullptr : (const float4*)mir.spairs;
     static const bool force_ref = std::getenv("RT_FORCE_REFERENCE_LAYOUT") != nullptr;  // A/B switch
     a.tris = force_ref ? nullptr : (const FlatTri*)tris;
     const bool stats = (p->flags & RT_RENDER_STATS) != 0;
