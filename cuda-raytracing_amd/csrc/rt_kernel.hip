@@ -781,17 +781,23 @@ hipError_t launch_fast_t(const RenderArgs& args, int tiles, hipStream_t stream) 
 
     // statistics: the reference's work on scalar records (RT_TUNE bit 7: through the leaf trees);
     // RT_TUNE bit 8: a timing frame of the production kernel instead (phase clocks, no counts)
-    if (STATS && (args.tune & 256u)) return launch_fast_m<STACK, false, 9>(args, tiles, stream);
+    if (STATS && (args.tune & 256u))
+        return (args.tune & 4096u) ? launch_fast_m<STACK, false, 9>(args, tiles, stream)
+                                   : launch_fast_m<STACK, false, 25>(args, tiles, stream);
     if (STATS) return (args.tree && (args.tune & 128u)) ? launch_fast_m<STACK, STATS, 6>(args, tiles, stream)
                                                         : launch_fast_m<STACK, STATS, 2>(args, tiles, stream);
     // big leaves: packed pairs in the shared-leaf loop, scalar records in cooperative rounds
     // (MODE 1, measured best), leaf trees compiled in only for scenes that have them (MODE 5);
     // A/B: RT_TUNE bits 4-5 = 2 scalar only, 3 pairs everywhere
-    if (args.tree) return launch_fast_m<STACK, STATS, 5>(args, tiles, stream);
+    // MODE bit 4: inner-node and small-leaf steps in separate iterations (rt_fast.h trace);
+    // RT_TUNE bit 12 turns it off (A/B)
+    const bool split = (args.tune & 4096u) == 0;
+    if (args.tree) return split ? launch_fast_m<STACK, STATS, 21>(args, tiles, stream)
+                                : launch_fast_m<STACK, STATS, 5>(args, tiles, stream);
     const uint32_t mode = (args.tune >> 4) & 3u;
     if (mode == 2) return launch_fast_m<STACK, STATS, 2>(args, tiles, stream);
     if (mode == 3) return launch_fast_m<STACK, STATS, 0>(args, tiles, stream);
-    return launch_fast_m<STACK, STATS, 1>(args, tiles, stream);
+    return split ? launch_fast_m<STACK, STATS, 17>(args, tiles, stream) : launch_fast_m<STACK, STATS, 1>(args, tiles, stream);
 }
 
 hipError_t launch_fast(const RenderArgs& args, int tiles, int depth, bool stats, hipStream_t s) {
