@@ -213,3 +213,58 @@ uint32_t rt_build_leaf_tree(const float* recs, uint32_t count, const LeafTreePar
     B.fill(root, all, false, ~0u);
     return root;
 }
+
+void rt_build_leaf_flat(std::vector<float>& nodes, uint32_t root, const LeafTreeParams& prm, std::vector<float>& flat) {
+    auto u32 = [&](uint32_t k, int f) {
+        uint32_t v;
+        std::memcpy(&v, &nodes[(size_t)k * 16 + f], 4);
+        return v;
+    };
+    auto put = [](float* rec, int f, uint32_t v) { std::memcpy(&rec[f], &v, 4); };
+    const uint32_t end = u32(root, 13);
+    // clusters in pre-order; first_cluster[k - root] = clusters before node k
+    std::vector<uint32_t> first_cluster(end - root + 1, 0);
+    const uint32_t cbase = (uint32_t)(flat.size() / 16);
+    uint32_t nc = 0;
+    for (uint32_t k = root; k < end; k++) {
+        first_cluster[k - root] = nc;
+        if (u32(k, 14) != ~0u) {
+            const size_t o = flat.size();
+            flat.insert(flat.end(), &nodes[(size_t)k * 16], &nodes[(size_t)k * 16] + 16);
+            put(&flat[o], 13, cbase + nc + 1);
+            nc++;
+        }
+    }
+    first_cluster[end - root] = nc;
+    const uint32_t kbase = (uint32_t)(flat.size() / 16);
+    uint32_t nk = 0;
+    std::vector<uint32_t> todo{root};
+    std::vector<uint32_t> cuts;
+    while (!todo.empty()) {  // pre-order cut: subtrees of at most cut_clusters clusters
+        const uint32_t k = todo.back();
+        todo.pop_back();
+        const uint32_t skip = u32(k, 13);
+        const uint32_t c0 = first_cluster[k - root], c1 = first_cluster[skip - root];
+        if (c1 == c0) continue;
+        if (c1 - c0 <= prm.cut_clusters || u32(k, 14) != ~0u) {
+            cuts.push_back(k);
+            continue;
+        }
+        std::vector<uint32_t> ch;
+        for (uint32_t c = k + 1; c < skip; c = u32(c, 13)) ch.push_back(c);
+        for (auto it = ch.rbegin(); it != ch.rend(); ++it) todo.push_back(*it);
+    }
+    for (uint32_t k : cuts) {
+        const size_t o = flat.size();
+        flat.insert(flat.end(), &nodes[(size_t)k * 16], &nodes[(size_t)k * 16] + 16);
+        put(&flat[o], 13, first_cluster[k - root]);
+        put(&flat[o], 14, first_cluster[u32(k, 13) - root]);
+        nk++;
+    }
+    float* R = &nodes[(size_t)root * 16];
+    put(R, 8, cbase);
+    put(R, 9, nc);
+    put(R, 10, kbase);
+    put(R, 11, nk);
+    put(R, 15, u32(root, 15) | 2u);
+}

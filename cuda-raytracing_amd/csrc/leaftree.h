@@ -19,6 +19,15 @@
 // Boxes and cones are rounded outward, so they bound the exact fp32 triangles.  tri_begin
 // indexes the leaf-tree triangle records (FlatTri with C.z = position in the leaf), ~0 for
 // inner nodes.
+//
+// Flat lists for the cooperative walk (rt_fast.h coop_tree), appended to a separate array:
+//   clusters  copies of the tree's cluster nodes in pre-order (K3.y = own index + 1);
+//   cuts      a cut of the tree into subtrees of at most LeafTreeParams::cut_clusters clusters:
+//             copies of those nodes with K3.y = first cluster, K3.z = end cluster (the
+//             subtree's clusters are contiguous in pre-order).
+// The root records where they are: K2 = (cluster base, cluster count, cut base, cut count) in
+// 16-float units of the flat array (uint bits) and info bit 1 set; the root is never culled, so
+// its cone fields are free.
 #pragma once
 
 #include <cstdint>
@@ -29,9 +38,14 @@ struct LeafTreeParams {
     double split_angle = 0.6;     // split by normals while the cone half-angle exceeds this (rad)
     double min_cull_cos = 0.05;   // nodes with a wider cone are never tested (always entered)
     double big_fraction = 0.25;   // triangles spanning this much of the leaf sit apart, untested
+    uint32_t cut_clusters = 32;   // clusters per subtree of the flat cut list
 };
 
 // Appends the tree for `count` FlatTri records (12 floats each) to `nodes` (16 floats per
 // node) and the reordered records to `ltris`; returns the root's node index.
 uint32_t rt_build_leaf_tree(const float* recs, uint32_t count, const LeafTreeParams& prm, std::vector<float>& nodes,
                             std::vector<float>& ltris);
+
+// Appends the flat cluster and cut lists of the tree rooted at `root` to `flat` (16 floats per
+// record) and records their place in the root (see above).
+void rt_build_leaf_flat(std::vector<float>& nodes, uint32_t root, const LeafTreeParams& prm, std::vector<float>& flat);

@@ -49,6 +49,7 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
     out->pairs.clear();
     out->tree.clear();
     out->ltris.clear();
+    out->flat.clear();
     out->depth = 0;
     out->fast = true;
     std::vector<uint32_t> big;
@@ -98,6 +99,7 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
         if (nd.prim_count >= tree_min) {
             po = rt_build_leaf_tree(&out->tris[(size_t)nd.first_index * 12], nd.prim_count, LeafTreeParams{}, out->tree,
                                     out->ltris);
+            rt_build_leaf_flat(out->tree, po, LeafTreeParams{}, out->flat);
             pf = 2;
             std::memcpy(&lead[10], &po, 4);
             std::memcpy(&lead[11], &pf, 4);
@@ -138,14 +140,15 @@ void release(Entry& e) {
 
 int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owned, uint64_t fingerprint) {
     const size_t nt = m.tris.size() * 4, np = m.pairs.size() * 4, nk = m.tree.size() * 4, nl = m.ltris.size() * 4,
-                 ns = m.spairs.size() * 4;
+                 ns = m.spairs.size() * 4, nf = m.flat.size() * 4;
     void* block = nullptr;
-    if (rt_malloc(&block, nt + np + nk + nl + ns + 64) != 0) return -1;
+    if (rt_malloc(&block, nt + np + nk + nl + ns + nf + 64) != 0) return -1;
     char* b = static_cast<char*>(block);
     if ((nt && rt_memcpy_h2d(b, m.tris.data(), nt) != 0) || (np && rt_memcpy_h2d(b + nt, m.pairs.data(), np) != 0) ||
         (nk && rt_memcpy_h2d(b + nt + np, m.tree.data(), nk) != 0) ||
         (nl && rt_memcpy_h2d(b + nt + np + nk, m.ltris.data(), nl) != 0) ||
-        (ns && rt_memcpy_h2d(b + nt + np + nk + nl, m.spairs.data(), ns) != 0)) {
+        (ns && rt_memcpy_h2d(b + nt + np + nk + nl, m.spairs.data(), ns) != 0) ||
+        (nf && rt_memcpy_h2d(b + nt + np + nk + nl + ns, m.flat.data(), nf) != 0)) {
         rt_free(block);
         return -1;
     }
@@ -155,6 +158,7 @@ int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owne
     e.dev.tree = nk ? b + nt + np : nullptr;
     e.dev.ltris = nl ? b + nt + np + nk : nullptr;
     e.dev.spairs = ns ? b + nt + np + nk + nl : nullptr;
+    e.dev.flat = nf ? b + nt + np + nk + nl + ns : nullptr;
     e.dev.depth = m.depth;
     e.dev.fast = m.fast;
     e.dev.owned = owned;

@@ -18,6 +18,7 @@
 //           records at other positions are unused;
 //  * tree / ltris  for leaves of at least MIRROR_TREE_LEAF triangles, a leaf tree instead
 //           (leaftree.h): the first record holds po = the root node, pf = 2;
+//  * flat   the leaf trees' flat cluster and cut lists (leaftree.h, cooperative walk);
 //  * depth  the deepest leaf (sizes the traversal stack) and whether every node bound lies in
 //           the range where the filtered slab test is proven (rt_fast.h).
 #pragma once
@@ -37,6 +38,7 @@ struct MirrorHost {
     std::vector<float> spairs;    // 20 floats per triangle position (small leaves' pairs)
     std::vector<float> tree;      // 16 floats per leaf-tree node
     std::vector<float> ltris;     // 12 floats per leaf-tree triangle record
+    std::vector<float> flat;      // 16 floats per record: leaf trees' flat cluster / cut lists
     int depth = 0;                // deepest leaf (root = 0) reachable from node 0
     bool fast = true;             // node bounds inside the filtered-slab range (rt_fast.h)
 };
@@ -55,6 +57,7 @@ struct MirrorDevice {
     const void* spairs = nullptr;
     const void* tree = nullptr;
     const void* ltris = nullptr;
+    const void* flat = nullptr;
     int depth = -1;
     bool fast = false;
     bool owned = true;         // built by rt_scene_upload, which forgets it before freeing the arrays

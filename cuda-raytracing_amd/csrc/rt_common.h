@@ -47,6 +47,7 @@ struct RenderArgs {
     const float4* tree;   // leaf trees of huge leaves (leaftree.h) or null
     const float4* ltris;  // their triangle records
     const float4* spairs; // small leaves' triangles in packed pairs, pair (i, i+1) at record i, or null
+    const float4* flat;   // leaf trees' flat cluster / cut lists (leaftree.h) or null
     uint32_t tune;  // A/B knobs (RT_TUNE, rt_render): bit0 no cooperative leaf rounds, bit1 no pair
                     // records, bit2 no leaf trees, bit3 no small-leaf pairs, bits 4-5 big-leaf mode (rt_kernel.hip launch_fast_t)
 };

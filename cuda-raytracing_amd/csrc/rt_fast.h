@@ -611,6 +611,134 @@ struct Trav {
     int sp;
 };
 
+// Cooperative walk of the leaf trees through their flat lists (leaftree.h) for the lanes `m`
+// waiting at tree leaves, one ray at a time: the whole wave screens the cut subtrees (a lane per
+// subtree), then the clusters of the surviving subtrees (a lane per cluster, two subtrees per
+// round), then the triangles of the surviving clusters (8 lanes per cluster, 8 clusters per
+// round).  cluster_cull excludes only what provably cannot pass the fp32 test with
+// 0 <= t < best; every lane keeps the (t, position) minimum of what it tested (leaf_candidate),
+// and the wave's (t, position) arg-min is exactly the sequential loop's result.  A NaN distance
+// sends the ray to the sequential loop.  The per-lane walk (tree_leaf) runs each lane's ray on
+// one lane, at a few percent lane utilisation; here all 64 lanes work on one ray.
+__device__ __forceinline__ f3 bcast3(f3 v, int lane) {
+    return rtm::mk(bcast(v.x, lane), bcast(v.y, lane), bcast(v.z, lane));
+}
+
+__device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree, const float4* ltris, const float4* flat,
+                                          unsigned long long m, uint32_t root_l, const Ray& R, Hit& h, const Trav& T) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const f3 rnd_l = rtm::mk(1.0f / R.nd.x, 1.0f / R.nd.y, 1.0f / R.nd.z);  // cluster_cull's reciprocals
+    while (m) {
+        const int r = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const uint32_t root = (uint32_t)__builtin_amdgcn_readlane((int)root_l, r);
+        const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)T.first, r);
+        const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)T.count, r);
+        Ray B;
+        B.o = bcast3(R.o, r);
+        B.nd = bcast3(R.nd, r);
+        B.d = B.nd, B.r = B.nd;  // unused by cluster_cull / leaf_candidate
+        B.fast = __builtin_amdgcn_readlane(R.fast ? 1 : 0, r) != 0;
+        const f3 rnd = bcast3(rnd_l, r);
+        const float best = bcast(h.best, r);
+        const f4v K2 = ((ConstF4)(tree + 4 * (size_t)root))[2];
+        const uint32_t cb = __float_as_uint(K2.x), kb = __float_as_uint(K2.z), nk = __float_as_uint(K2.w);
+        const float4* cl = flat + 4 * (size_t)cb;
+        const float4* ct = flat + 4 * (size_t)kb;
+        LeafBest L;
+        L.t = best, L.j = 0, L.id = 0, L.bx = 0.0f, L.by = 0.0f, L.found = false;
+        L.nan = !(best == best);
+        const bool cull_ok = B.fast && !L.nan;
+        for (uint32_t kbase = 0; kbase < nk; kbase += 64u) {
+            const uint32_t k = kbase + lane;
+            bool need = false;
+            uint32_t s0 = 0, s1 = 0;
+            if (k < nk) {
+                const float4 K3 = ct[4 * k + 3];
+                s0 = __float_as_uint(K3.y), s1 = __float_as_uint(K3.z);
+                need = !(cull_ok && (__float_as_uint(K3.w) & 1u) &&
+                         cluster_cull(B, rnd, best, ct[4 * k], ct[4 * k + 1], ct[4 * k + 2], K3));
+            }
+            unsigned long long mk = __ballot(need);
+            while (mk) {
+                const int a = __ffsll((long long)mk) - 1;
+                mk &= mk - 1;
+                int b = -1;
+                if (mk) {
+                    b = __ffsll((long long)mk) - 1;
+                    mk &= mk - 1;
+                }
+                const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)s0, a);
+                const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)s1, a);
+                uint32_t b0 = 0, b1 = 0;
+                if (b >= 0) {
+                    b0 = (uint32_t)__builtin_amdgcn_readlane((int)s0, b);
+                    b1 = (uint32_t)__builtin_amdgcn_readlane((int)s1, b);
+                }
+                const uint32_t c = lane < 32u ? a0 + lane : b0 + (lane - 32u);
+                const bool has = lane < 32u ? c < a1 : c < b1;
+                bool need2 = false;
+                uint32_t tb = 0, n = 0;
+                if (has) {
+                    const float4 Q3 = cl[4 * c + 3];
+                    const uint32_t info = __float_as_uint(Q3.w);
+                    tb = __float_as_uint(Q3.z), n = info >> 8;
+                    need2 = !(cull_ok && (info & 1u) && cluster_cull(B, rnd, best, cl[4 * c], cl[4 * c + 1], cl[4 * c + 2], Q3));
+                }
+                unsigned long long mc = __ballot(need2);
+                while (mc) {
+                    const uint32_t g = lane >> 3, i = lane & 7u;
+                    uint32_t my_tb = 0, my_n = 0;
+                    for (uint32_t q = 0; q < 8u && mc; q++) {
+                        const int sl = __ffsll((long long)mc) - 1;
+                        mc &= mc - 1;
+                        const uint32_t tq = (uint32_t)__builtin_amdgcn_readlane((int)tb, sl);
+                        const uint32_t nq = (uint32_t)__builtin_amdgcn_readlane((int)n, sl);
+                        if (g == q) my_tb = tq, my_n = nq;
+                    }
+                    if (i < my_n) {
+                        const size_t t3 = 3 * (size_t)(my_tb + i);
+                        leaf_candidate(B, ltris[t3], ltris[t3 + 1], ltris[t3 + 2], L);
+                    }
+                }
+            }
+        }
+        if (__ballot(L.nan)) {
+            // sequential fallback for this ray (never taken for finite scenes)
+            if ((int)lane == r) {
+                for (uint32_t q = f0; q < f0 + c0; q++) {
+                    float t, x, y;
+                    bool dummy = false;
+                    const float4 A = tris[3 * q], Bq = tris[3 * q + 1], Cc = tris[3 * q + 2];
+                    if (tri_accept(R.o, R.nd, A, Bq, Cc, h.best, &t, &x, &y, &dummy)) {
+                        h.best = t, h.kind = 2, h.bx = x, h.by = y;
+                        h.id = __float_as_uint(Cc.y);
+                    }
+                }
+            }
+            continue;
+        }
+        // arg-min of (t, position) over the lanes holding a candidate
+        float mt = L.found ? L.t : __int_as_float(0x7f800000);
+        uint32_t mj = L.found ? L.j : 0xffffffffu;
+        for (int off = 32; off > 0; off >>= 1) {
+            const float ot = __shfl_xor(mt, off);
+            const uint32_t oj = (uint32_t)__shfl_xor((int)mj, off);
+            const bool take = ot < mt || (ot == mt && oj < mj);
+            mt = take ? ot : mt;
+            mj = take ? oj : mj;
+        }
+        mj = __builtin_amdgcn_readfirstlane(mj);
+        if (mj != 0xffffffffu) {
+            const int wl = __ffsll((long long)__ballot(L.found && L.j == mj)) - 1;
+            const float wt = bcast(L.t, wl), wbx = bcast(L.bx, wl), wby = bcast(L.by, wl);
+            const uint32_t wid = (uint32_t)__builtin_amdgcn_readlane((int)L.id, wl);
+            if ((int)lane == r) h.best = wt, h.kind = 2, h.id = wid, h.bx = wbx, h.by = wby;
+        }
+    }
+}
+
+
 // IntersectAABB of the root against the closest sphere distance (main_raytracing.cu:37-45):
 // whether the lane has anything to traverse.
 template <bool STATS, class C>
@@ -650,7 +778,8 @@ __device__ __forceinline__ bool small_step(const float4* nodes4, const float4* t
 // lane ran its leaf (it then pops; the others keep waiting).
 template <bool STATS, int MODE, class C>
 __device__ __forceinline__ bool big_round(const float4* tris, const float4* pairs, const float4* tree,
-                                          const float4* ltris, uint32_t tune, unsigned long long big, bool waiting,
+                                          const float4* ltris, const float4* flat, uint32_t tune,
+                                          unsigned long long big, bool waiting,
                                           const Ray& R, Hit& h, const Trav& T, C& c) {
     if ((MODE & 4) && tree) {  // MODE bit 2: the scene has leaf trees
         // lanes at leaves with a leaf tree (mirror.h: lead record pf == 2) walk it on their own
@@ -661,8 +790,12 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
             at_tree = __float_as_uint(lead.w) == 2u;
             root = __float_as_uint(lead.z);
         }
-        if (__ballot(at_tree)) {
-            if (at_tree) tree_leaf<STATS>(tris, tree, ltris, root, T.first, T.count, R, h, c);
+        const unsigned long long mt = __ballot(at_tree);
+        if (mt) {
+            if (!STATS && flat && (tune & 8192u) == 0)  // RT_TUNE bit 13: per-lane walk instead
+                coop_tree(tris, tree, ltris, flat, mt, root, R, h, T);
+            else if (at_tree)
+                tree_leaf<STATS>(tris, tree, ltris, root, T.first, T.count, R, h, c);
             return at_tree;
         }
     }
@@ -731,7 +864,8 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
 // reference's triangle tests plus the tree's own work).
 template <bool STATS, int MODE, class C>
 __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, const float4* pairs,
-                                      const float4* tree, const float4* ltris, const float4* spairs, uint32_t tune,
+                                      const float4* tree, const float4* ltris, const float4* flat,
+                                      const float4* spairs, uint32_t tune,
                                       uint32_t* stk,
                                       const Ray& R, Hit& h, bool live, C& c) {
     Trav T{0, 0, 0};
@@ -780,7 +914,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
         }
         const unsigned long long big = __ballot(active);
         if (!big) break;
-        if (big_round<STATS, MODE>(tris, pairs, tree, ltris, tune, big, active, R, h, T, c))
+        if (big_round<STATS, MODE>(tris, pairs, tree, ltris, flat, tune, big, active, R, h, T, c))
             active = pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
         if (TIMING) {
             const unsigned long long t1 = __builtin_amdgcn_s_memtime();

@@ -594,7 +594,8 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
             }
         }
         const rtfast::Ray R = rtfast::make_ray(ro, rd, nd, scene_fast);
-        rtfast::trace<STATS, MODE>(nodes4, tris, a.pairs, a.tree, a.ltris, a.spairs, a.tune, stk, R, h, path, c);
+        rtfast::trace<STATS, MODE>(nodes4, tris, a.pairs, a.tree, a.ltris, a.flat, a.spairs, a.tune, stk, R, h, path,
+                                   c);
         if (!path) continue;
 
         bool end = shade_segment<STATS>(a, h, ro, rd, nd, rng, color, thr, c);
@@ -990,6 +991,7 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     a.tree = (a.tune & 4u) ? nullptr : (const float4*)mir.tree;
     a.ltris = (const float4*)mir.ltris;
     a.spairs = (a.tune & 8u) ? nullptr : (const float4*)mir.spairs;
+    a.flat = (const float4*)mir.flat;
     static const bool force_ref = std::getenv("RT_FORCE_REFERENCE_LAYOUT") != nullptr;  // A/B switch
     a.tris = force_ref ? nullptr : (const FlatTri*)tris;
     const bool stats = (p->flags & RT_RENDER_STATS) != 0;
