@@ -38,7 +38,7 @@ struct LeafTreeParams {
     double split_angle = 0.6;     // split by normals while the cone half-angle exceeds this (rad)
     double min_cull_cos = 0.05;   // nodes with a wider cone are never tested (always entered)
     double big_fraction = 0.25;   // triangles spanning this much of the leaf sit apart, untested
-    uint32_t cut_clusters = 32;   // clusters per subtree of the flat cut list
+    uint32_t cut_clusters = 32;   // clusters per subtree of the flat cut list (<= 32: rt_fast.h coop_tree)
 };
 
 // Appends the tree for `count` FlatTri records (12 floats each) to `nodes` (16 floats per

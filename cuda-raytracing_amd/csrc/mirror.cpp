@@ -97,9 +97,14 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
             return e ? (uint32_t)std::strtoul(e, nullptr, 0) : MIRROR_TREE_LEAF;
         }();
         if (nd.prim_count >= tree_min) {
-            po = rt_build_leaf_tree(&out->tris[(size_t)nd.first_index * 12], nd.prim_count, LeafTreeParams{}, out->tree,
-                                    out->ltris);
-            rt_build_leaf_flat(out->tree, po, LeafTreeParams{}, out->flat);
+            static const LeafTreeParams prm = [] {
+                LeafTreeParams p;
+                const char* e = std::getenv("RT_CUT_CLUSTERS");  // tuning
+                if (e) p.cut_clusters = std::min<uint32_t>(32u, (uint32_t)std::strtoul(e, nullptr, 0));
+                return p;
+            }();
+            po = rt_build_leaf_tree(&out->tris[(size_t)nd.first_index * 12], nd.prim_count, prm, out->tree, out->ltris);
+            rt_build_leaf_flat(out->tree, po, prm, out->flat);
             pf = 2;
             std::memcpy(&lead[10], &po, 4);
             std::memcpy(&lead[11], &pf, 4);

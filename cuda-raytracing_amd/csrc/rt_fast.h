@@ -613,9 +613,9 @@ struct Trav {
 
 // Cooperative walk of the leaf trees through their flat lists (leaftree.h) for the lanes `m`
 // waiting at tree leaves, one ray at a time: the whole wave screens the cut subtrees (a lane per
-// subtree), then the clusters of the surviving subtrees (a lane per cluster, two subtrees per
-// round), then the triangles of the surviving clusters (8 lanes per cluster, 8 clusters per
-// round).  cluster_cull excludes only what provably cannot pass the fp32 test with
+// subtree), then -- nearest box first -- the clusters of the surviving subtrees (a lane per
+// cluster, two subtrees per round), then the triangles of the surviving clusters (8 lanes per
+// cluster, 8 clusters per round); the cull bound drops to the best candidate found so far.  cluster_cull excludes only what provably cannot pass the fp32 test with
 // 0 <= t < best; every lane keeps the (t, position) minimum of what it tested (leaf_candidate),
 // and the wave's (t, position) arg-min is exactly the sequential loop's result.  A NaN distance
 // sends the ray to the sequential loop.  The per-lane walk (tree_leaf) runs each lane's ray on
@@ -624,13 +624,16 @@ __device__ __forceinline__ f3 bcast3(f3 v, int lane) {
     return rtm::mk(bcast(v.x, lane), bcast(v.y, lane), bcast(v.z, lane));
 }
 
+template <bool TIMING, class C>
 __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree, const float4* ltris, const float4* flat,
-                                          unsigned long long m, uint32_t root_l, const Ray& R, Hit& h, const Trav& T) {
+                                          unsigned long long m, uint32_t root_l, const Ray& R, Hit& h, const Trav& T,
+                                          uint32_t* scratch, C& c) {
     const uint32_t lane = threadIdx.x & 63u;
     const f3 rnd_l = rtm::mk(1.0f / R.nd.x, 1.0f / R.nd.y, 1.0f / R.nd.z);  // cluster_cull's reciprocals
     while (m) {
         const int r = __ffsll((long long)m) - 1;
         m &= m - 1;
+        if (TIMING && lane == 0) c.r_coop++;
         const uint32_t root = (uint32_t)__builtin_amdgcn_readlane((int)root_l, r);
         const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)T.first, r);
         const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)T.count, r);
@@ -649,25 +652,37 @@ __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree
         L.t = best, L.j = 0, L.id = 0, L.bx = 0.0f, L.by = 0.0f, L.found = false;
         L.nan = !(best == best);
         const bool cull_ok = B.fast && !L.nan;
+        float cbest = best;  // cull bound: next float above the best candidate found so far
         for (uint32_t kbase = 0; kbase < nk; kbase += 64u) {
             const uint32_t k = kbase + lane;
             bool need = false;
             uint32_t s0 = 0, s1 = 0;
+            float te = 0.0f;
             if (k < nk) {
-                const float4 K3 = ct[4 * k + 3];
+                const float4 K0 = ct[4 * k], K1 = ct[4 * k + 1], K3 = ct[4 * k + 3];
                 s0 = __float_as_uint(K3.y), s1 = __float_as_uint(K3.z);
-                need = !(cull_ok && (__float_as_uint(K3.w) & 1u) &&
-                         cluster_cull(B, rnd, best, ct[4 * k], ct[4 * k + 1], ct[4 * k + 2], K3));
+                need = !(cull_ok && (__float_as_uint(K3.w) & 1u) && cluster_cull(B, rnd, cbest, K0, K1, ct[4 * k + 2], K3));
+                // box entry distance along the ray, only to visit near subtrees first
+                const float tx1 = (K0.x - B.o.x) * rnd.x, tx2 = (K1.x - B.o.x) * rnd.x;
+                const float ty1 = (K0.y - B.o.y) * rnd.y, ty2 = (K1.y - B.o.y) * rnd.y;
+                const float tz1 = (K0.z - B.o.z) * rnd.z, tz2 = (K1.z - B.o.z) * rnd.z;
+                te = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+                te = te == te ? te : 0.0f;
             }
-            unsigned long long mk = __ballot(need);
-            while (mk) {
-                const int a = __ffsll((long long)mk) - 1;
-                mk &= mk - 1;
-                int b = -1;
-                if (mk) {
-                    b = __ffsll((long long)mk) - 1;
-                    mk &= mk - 1;
-                }
+            const unsigned long long mk = __ballot(need);
+            const uint32_t ns = (uint32_t)__popcll(mk);
+            if (TIMING && lane == 0) c.ktest += min(64u, nk - kbase), c.r_shared += ns;
+            // near-first order of the surviving subtrees: rank by (entry distance, lane)
+            uint32_t rank = 0;
+            for (unsigned long long w = mk; w; w &= w - 1) {
+                const int b = __ffsll((long long)w) - 1;
+                const float tb = bcast(te, b);
+                rank += (tb < te || (tb == te && b < (int)lane)) ? 1u : 0u;
+            }
+            for (uint32_t q = 0; q < ns; q += 2) {
+                // two subtrees per round (<= 32 clusters each): lanes 0-31 and 32-63
+                const int a = __ffsll((long long)__ballot(need && rank == q)) - 1;
+                const int b = q + 1 < ns ? __ffsll((long long)__ballot(need && rank == q + 1)) - 1 : -1;
                 const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)s0, a);
                 const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)s1, a);
                 uint32_t b0 = 0, b1 = 0;
@@ -675,31 +690,45 @@ __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree
                     b0 = (uint32_t)__builtin_amdgcn_readlane((int)s0, b);
                     b1 = (uint32_t)__builtin_amdgcn_readlane((int)s1, b);
                 }
-                const uint32_t c = lane < 32u ? a0 + lane : b0 + (lane - 32u);
-                const bool has = lane < 32u ? c < a1 : c < b1;
+                const uint32_t ci = lane < 32u ? a0 + lane : b0 + (lane - 32u);
+                const bool has = lane < 32u ? ci < a1 : ci < b1;
                 bool need2 = false;
                 uint32_t tb = 0, n = 0;
                 if (has) {
-                    const float4 Q3 = cl[4 * c + 3];
+                    const float4 Q3 = cl[4 * ci + 3];
                     const uint32_t info = __float_as_uint(Q3.w);
                     tb = __float_as_uint(Q3.z), n = info >> 8;
-                    need2 = !(cull_ok && (info & 1u) && cluster_cull(B, rnd, best, cl[4 * c], cl[4 * c + 1], cl[4 * c + 2], Q3));
+                    need2 = !(cull_ok && (info & 1u) && cluster_cull(B, rnd, cbest, cl[4 * ci], cl[4 * ci + 1], cl[4 * ci + 2], Q3));
                 }
-                unsigned long long mc = __ballot(need2);
-                while (mc) {
-                    const uint32_t g = lane >> 3, i = lane & 7u;
-                    uint32_t my_tb = 0, my_n = 0;
-                    for (uint32_t q = 0; q < 8u && mc; q++) {
-                        const int sl = __ffsll((long long)mc) - 1;
-                        mc &= mc - 1;
-                        const uint32_t tq = (uint32_t)__builtin_amdgcn_readlane((int)tb, sl);
-                        const uint32_t nq = (uint32_t)__builtin_amdgcn_readlane((int)n, sl);
-                        if (g == q) my_tb = tq, my_n = nq;
+                const unsigned long long mc = __ballot(need2);
+                const uint32_t nsc = (uint32_t)__popcll(mc);
+                if (TIMING && lane == 0) c.l_big++, c.ktest += __popcll(__ballot(has)), c.coop_rays += nsc;
+                // surviving clusters, compacted in order through the wave's LDS scratch
+                if (need2) {
+                    const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(mc >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mc, 0u));
+                    scratch[rk] = tb, scratch[64 + rk] = n;
+                }
+                __builtin_amdgcn_wave_barrier();
+                for (uint32_t base = 0; base < nsc; base += 8u) {
+                    if (TIMING && lane == 0) c.w_big++;
+                    const uint32_t slot = base + (lane >> 3), i = lane & 7u;
+                    if (slot < nsc) {
+                        const uint32_t my_tb = scratch[slot], my_n = scratch[64 + slot];
+                        if (i < my_n) {
+                            const size_t t3 = 3 * (size_t)(my_tb + i);
+                            leaf_candidate(B, ltris[t3], ltris[t3 + 1], ltris[t3 + 2], L);
+                        }
                     }
-                    if (i < my_n) {
-                        const size_t t3 = 3 * (size_t)(my_tb + i);
-                        leaf_candidate(B, ltris[t3], ltris[t3 + 1], ltris[t3 + 2], L);
-                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                // tighten the cull bound to just above the best candidate so far (ties on t are
+                // decided by position, so a triangle at exactly that distance must stay in)
+                if (__ballot(L.found)) {
+                    float mt = L.found ? L.t : __int_as_float(0x7f800000);
+                    for (int off = 32; off > 0; off >>= 1) mt = fminf(mt, __shfl_xor(mt, off));
+                    mt = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(mt)));
+                    const float up = __uint_as_float(__float_as_uint(mt) + 1u);  // mt >= 0, finite
+                    cbest = fminf(cbest, up);
                 }
             }
         }
@@ -778,7 +807,7 @@ __device__ __forceinline__ bool small_step(const float4* nodes4, const float4* t
 // lane ran its leaf (it then pops; the others keep waiting).
 template <bool STATS, int MODE, class C>
 __device__ __forceinline__ bool big_round(const float4* tris, const float4* pairs, const float4* tree,
-                                          const float4* ltris, const float4* flat, uint32_t tune,
+                                          const float4* ltris, const float4* flat, uint32_t* scratch, uint32_t tune,
                                           unsigned long long big, bool waiting,
                                           const Ray& R, Hit& h, const Trav& T, C& c) {
     if ((MODE & 4) && tree) {  // MODE bit 2: the scene has leaf trees
@@ -793,7 +822,7 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
         const unsigned long long mt = __ballot(at_tree);
         if (mt) {
             if (!STATS && flat && (tune & 8192u) == 0)  // RT_TUNE bit 13: per-lane walk instead
-                coop_tree(tris, tree, ltris, flat, mt, root, R, h, T);
+                coop_tree<(MODE & 8) != 0>(tris, tree, ltris, flat, mt, root, R, h, T, scratch, c);
             else if (at_tree)
                 tree_leaf<STATS>(tris, tree, ltris, root, T.first, T.count, R, h, c);
             return at_tree;
@@ -865,8 +894,7 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
 template <bool STATS, int MODE, class C>
 __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, const float4* pairs,
                                       const float4* tree, const float4* ltris, const float4* flat,
-                                      const float4* spairs, uint32_t tune,
-                                      uint32_t* stk,
+                                      const float4* spairs, uint32_t tune, uint32_t* stk, uint32_t* scratch,
                                       const Ray& R, Hit& h, bool live, C& c) {
     Trav T{0, 0, 0};
     bool active = live && trav_begin<STATS>(nodes4, R, h, T, c);
@@ -914,7 +942,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
         }
         const unsigned long long big = __ballot(active);
         if (!big) break;
-        if (big_round<STATS, MODE>(tris, pairs, tree, ltris, flat, tune, big, active, R, h, T, c))
+        if (big_round<STATS, MODE>(tris, pairs, tree, ltris, flat, scratch, tune, big, active, R, h, T, c))
             active = pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
         if (TIMING) {
             const unsigned long long t1 = __builtin_amdgcn_s_memtime();

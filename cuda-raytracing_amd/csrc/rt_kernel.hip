@@ -496,7 +496,7 @@ __device__ __forceinline__ bool shade_segment(const RenderArgs& a, const rtfast:
 // the bounce limit, start its next sample -- so a lane only idles once its whole pixel is
 // done.  The per-pixel draw order (u, v, then 4 draws per hit) is the reference's.
 template <int STACK, bool STATS, int MODE>
-__device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* const stk) {
+__device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* const stk, uint32_t* const scratch) {
     const float4* nodes4 = reinterpret_cast<const float4*>(a.nodes);
     const float4* tris = reinterpret_cast<const float4*>(a.tris);
     // one 64-lane workgroup per 8x8 sub-tile: tile k = blockIdx / 4, sub-tile blockIdx % 4
@@ -594,8 +594,8 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
             }
         }
         const rtfast::Ray R = rtfast::make_ray(ro, rd, nd, scene_fast);
-        rtfast::trace<STATS, MODE>(nodes4, tris, a.pairs, a.tree, a.ltris, a.flat, a.spairs, a.tune, stk, R, h, path,
-                                   c);
+        rtfast::trace<STATS, MODE>(nodes4, tris, a.pairs, a.tree, a.ltris, a.flat, a.spairs, a.tune, stk, scratch, R, h,
+                                   path, c);
         if (!path) continue;
 
         bool end = shade_segment<STATS>(a, h, ro, rd, nd, rng, color, thr, c);
@@ -628,6 +628,11 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
         atomicAdd(a.stats + RT_STAT_ROUNDS_COOP, c.r_coop);
         atomicAdd(a.stats + RT_STAT_ROUNDS_SHARED, c.r_shared);
         atomicAdd(a.stats + RT_STAT_COOP_RAYS, c.coop_rays);
+        // cooperative leaf-tree walk (wave-level): rays, subtree + cluster tests, triangle rounds
+        atomicAdd(a.stats + RT_STAT_TREE_NODES, c.ktest);
+        atomicAdd(a.stats + RT_STAT_TREE_TRI_TESTS, c.ktri);
+        atomicAdd(a.stats + RT_STAT_WAVE_BIG_TRIS, c.w_big);
+        atomicAdd(a.stats + RT_STAT_LANE_BIG_TRIS, c.l_big);
         // RT_TUNE bit 11: per-wave clocks (start, end) after the counters, for load-balance analysis
         if (a.tune & 2048u) {
             unsigned long long* w = a.stats + RT_STAT_COUNT + 8 * (size_t)blockIdx.x;
@@ -666,17 +671,20 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
 template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
     __shared__ uint32_t stack_lds[STACK * WAVE];  // one word per entry (rt_fast.h pop)
-    render_fast_body<STACK, STATS, MODE>(a, stack_lds + threadIdx.x);
+    __shared__ uint32_t scratch_lds[(MODE & 4) ? 128 : 1];  // coop_tree's cluster compaction
+    render_fast_body<STACK, STATS, MODE>(a, stack_lds + threadIdx.x, scratch_lds);
 }
 template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(5))) void render_fast_kernel_w5(RenderArgs a) {
     __shared__ uint32_t stack_lds[STACK * WAVE];
-    render_fast_body<STACK, STATS, MODE>(a, stack_lds + threadIdx.x);
+    __shared__ uint32_t scratch_lds[(MODE & 4) ? 128 : 1];  // coop_tree's cluster compaction
+    render_fast_body<STACK, STATS, MODE>(a, stack_lds + threadIdx.x, scratch_lds);
 }
 template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(6))) void render_fast_kernel_w6(RenderArgs a) {
     __shared__ uint32_t stack_lds[STACK * WAVE];
-    render_fast_body<STACK, STATS, MODE>(a, stack_lds + threadIdx.x);
+    __shared__ uint32_t scratch_lds[(MODE & 4) ? 128 : 1];  // coop_tree's cluster compaction
+    render_fast_body<STACK, STATS, MODE>(a, stack_lds + threadIdx.x, scratch_lds);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -783,8 +791,9 @@ hipError_t launch_fast_t(const RenderArgs& args, int tiles, hipStream_t stream) 
     // statistics: the reference's work on scalar records (RT_TUNE bit 7: through the leaf trees);
     // RT_TUNE bit 8: a timing frame of the production kernel instead (phase clocks, no counts)
     if (STATS && (args.tune & 256u))
-        return (args.tune & 4096u) ? launch_fast_m<STACK, false, 9>(args, tiles, stream)
-                                   : launch_fast_m<STACK, false, 25>(args, tiles, stream);
+        return args.tree ? launch_fast_m<STACK, false, 29>(args, tiles, stream)
+               : (args.tune & 4096u) ? launch_fast_m<STACK, false, 9>(args, tiles, stream)
+                                     : launch_fast_m<STACK, false, 25>(args, tiles, stream);
     if (STATS) return (args.tree && (args.tune & 128u)) ? launch_fast_m<STACK, STATS, 6>(args, tiles, stream)
                                                         : launch_fast_m<STACK, STATS, 2>(args, tiles, stream);
     // big leaves: packed pairs in the shared-leaf loop, scalar records in cooperative rounds
