@@ -27,10 +27,10 @@ ASSETS_DIR = os.path.join(ROOT_DIR, "assets")
 
 RT_RENDER_STATS = 1
 TRACERS = {"fast": 0, "ref": 2, "flat": 4}  # rt_render_params.flags
-STAT_NAMES = ("segments", "nodes", "tri_tests", "tri_accepts", "sphere_accepts", "hits", "misses", "",
+STAT_NAMES = ("segments", "nodes", "tri_tests", "tri_accepts", "sphere_accepts", "hits", "misses", "cycles_tree_cut",
               "wave_small_iters", "lane_small", "wave_big_tris", "lane_big_tris", "wave_segment_iters",
               "lane_segments", "tree_nodes", "tree_tri_tests", "cycles_small", "cycles_big", "cycles_total",
-              "rounds_coop", "rounds_shared", "coop_rays")
+              "rounds_coop", "rounds_shared", "coop_rays", "cycles_tree_clusters", "cycles_tree_tris")
 SCENES = {"bunny": 0, "bunny4": 1, "plane1m": 2}
 
 REFERENCE_SPP = 5      # main_raytracing.cu:166-170 (Release)

@@ -690,6 +690,7 @@ __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree
                     b0 = (uint32_t)__builtin_amdgcn_readlane((int)s0, b);
                     b1 = (uint32_t)__builtin_amdgcn_readlane((int)s1, b);
                 }
+                const unsigned long long tc0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
                 const uint32_t ci = lane < 32u ? a0 + lane : b0 + (lane - 32u);
                 const bool has = lane < 32u ? ci < a1 : ci < b1;
                 bool need2 = false;
@@ -703,6 +704,8 @@ __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree
                 const unsigned long long mc = __ballot(need2);
                 const uint32_t nsc = (uint32_t)__popcll(mc);
                 if (TIMING && lane == 0) c.l_big++, c.ktest += __popcll(__ballot(has)), c.coop_rays += nsc;
+                const unsigned long long tc1 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+                if (TIMING) c.cy_tcl += tc1 - tc0;
                 // surviving clusters, compacted in order through the wave's LDS scratch
                 if (need2) {
                     const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(mc >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mc, 0u));
@@ -721,6 +724,7 @@ __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
+                if (TIMING) c.cy_ttri += __builtin_amdgcn_s_memtime() - tc1;
                 // tighten the cull bound to just above the best candidate so far (ties on t are
                 // decided by position, so a triangle at exactly that distance must stay in)
                 if (__ballot(L.found)) {
