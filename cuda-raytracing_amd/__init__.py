@@ -113,6 +113,7 @@ SIGNATURES = {
     "rt_scene_host_arrays": (_SZ, [_P, ctypes.POINTER(_P), ctypes.POINTER(_SZ), ctypes.POINTER(_P),
                                    ctypes.POINTER(_SZ), ctypes.POINTER(_P), ctypes.POINTER(_SZ), ctypes.POINTER(_P)]),
     "rt_scene_bvh_max_depth": (_I, [_P]),
+    "rt_bvh_build_device": (_I, [_P, _U32, _P, _U32, _P, _P, ctypes.POINTER(_U32), ctypes.POINTER(_I), _P]),
     "rt_scene_mirror_info": (_I, [_P, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
     "rt_scene_mirror_copy": (_I, [_P, _P, _P, _P]),
     "rt_cluster_cull_host": (_I, [_P, _P, ctypes.c_float, _P]),
@@ -259,6 +260,21 @@ class Scene:
         nn, nf, nv = counts[0].value, counts[1].value, counts[2].value
         return {"nodes": grab(ptrs[0], nn * 32), "face_indices": grab(ptrs[1], nf * 4),
                 "vertices": grab(ptrs[2], nv * 32), "faces": grab(ptrs[3], nf * 16)}
+
+
+def bvh_build_device(vertices, faces, stream=None):
+    """BVH::Calculate on the GPU (rt_bvh_build_device) from device tensors of GPUVertex (N,8) f32
+    and GPUFace (F,4) u32 rows; returns (nodes (2F-1, 8) f32 device tensor, face_indices (F,) int32
+    device tensor, node_count, max_depth)."""
+    import torch
+    nf = faces.shape[0]
+    nodes = torch.empty((max(1, 2 * nf - 1), 8), dtype=torch.float32, device=faces.device)
+    fi = torch.empty((nf,), dtype=torch.int32, device=faces.device)
+    count, depth = _U32(0), _I(0)
+    _check(lib().rt_bvh_build_device(vertices.data_ptr(), vertices.shape[0], faces.data_ptr(), nf, nodes.data_ptr(),
+                                     fi.data_ptr(), ctypes.byref(count), ctypes.byref(depth), _stream_ptr(stream)),
+           "rt_bvh_build_device")
+    return nodes, fi, count.value, depth.value
 
 
 def alloc_surface(width, height, device=None):

@@ -28,7 +28,7 @@ ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 # fp32 division and square root (bit-exact agreement between host code, kernels and oracle).
 FP_FLAGS = ["-ffp-contract=off", "-fno-fast-math"]
 HOST_SOURCES = ["scene.cpp", "objload.cpp", "mirror.cpp", "leaftree.cpp", "xorwow.cpp", "image.cpp"]
-HIP_SOURCES = ["rt_kernel.hip", "image.hip"]
+HIP_SOURCES = ["rt_kernel.hip", "image.hip", "bvh_build.hip"]
 
 
 def _run(cmd):

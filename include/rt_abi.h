@@ -291,6 +291,15 @@ size_t rt_scene_host_arrays(const rt_scene* scene, const GPUBVHNode** nodes, siz
                             size_t* vertex_count, const GPUFace** faces);
 int rt_scene_bvh_max_depth(const rt_scene* scene);
 
+/* The reference's BVH builder (BVH::Calculate, RayTracing/BVH.cpp:8-124) run on the GPU over
+ * device arrays: nodes and face indices byte-identical to the host builder (depth-first node
+ * numbering, the swap partition's permutation including failed axes).  nodes_out holds
+ * 2 * face_count - 1 nodes; *node_count_out receives nodes_used, *max_depth_out the deepest level.
+ * Vertex positions must be finite.  Synchronises `stream`.  Returns 0 or an error code. */
+int rt_bvh_build_device(const GPUVertex* vertices, uint32_t vertex_count, const GPUFace* faces, uint32_t face_count,
+                        GPUBVHNode* nodes_out, uint32_t* face_indices_out, uint32_t* node_count_out,
+                        int* max_depth_out, void* stream);
+
 /* Diagnostics for the tests: the kernel's private triangle mirror (cuda-raytracing_amd/csrc/
    mirror.h: leaf-ordered records, 12 floats; leaf-tree nodes, 16 floats; leaf-tree triangle
    records, 12 floats) built on the host from the scene's host arrays, and the render kernel's
