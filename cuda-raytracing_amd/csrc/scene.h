@@ -85,6 +85,8 @@ class BVH {
     size_t GetNodeCount() const { return nodes_used; }
     const std::vector<uint32_t>& GetFaceIndices() const { return face_indices; }
     int GetMaxDepth() const { return max_depth; }
+    // adopt a build made elsewhere (rt_bvh_build_device, byte-identical to Calculate)
+    void Adopt(std::vector<GPUBVHNode> built_nodes, std::vector<uint32_t> built_face_indices, int depth);
 };
 
 // A triangle mesh as the reference receives it from assimp (aiMesh positions/normals/faces).
