@@ -24,6 +24,9 @@
 //    pre-order).  That count comes from subtree inner-node counts (bottom-up over the levels)
 //    and a top-down pass.
 //
+// Nodes of at most SMALL triangles build their whole subtree in one thread with the loop itself
+// (k_small_subtrees), which removes the deep levels' launches.
+//
 // Node bounds (UpdateBounds, glm::min / max from +-1e30) are tile reductions; min / max are
 // order-independent for finite coordinates, so the result is the sequential one.  Non-finite
 // vertex positions are rejected (the host builder handles those scenes).
@@ -31,6 +34,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -43,6 +47,7 @@ void rt_internal_set_error(const char* msg);
 namespace {
 
 constexpr int TS = 256;  // elements per tile = threads per workgroup
+constexpr uint32_t SMALL = 64;  // largest node that may build its whole subtree in one thread
 
 struct BNode {
     uint32_t first, count;
@@ -55,7 +60,7 @@ struct BNode {
     int32_t axes[3];
     float split;
     uint32_t nleft, p;
-    int32_t found;   // 1: split found at the current attempt, 2: found earlier
+    int32_t found;   // 0: still splitting, 1: split found, 2: leaf (one triangle), 3: small subtree
 };
 
 // element: centroid.xyz, face index bits
@@ -141,7 +146,7 @@ __global__ __launch_bounds__(TS) void k_bounds_tiles(const BNode* __restrict__ n
 }
 
 __global__ void k_bounds_nodes(BNode* __restrict__ nodes, const uint32_t* __restrict__ lvl, uint32_t nl,
-                               const uint32_t* __restrict__ tile_start, const float* __restrict__ part) {
+                               const uint32_t* __restrict__ tile_start, const float* __restrict__ part, uint32_t small) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nl) return;
     BNode& nd = nodes[lvl[i]];
@@ -164,7 +169,8 @@ __global__ void k_bounds_nodes(BNode* __restrict__ nodes, const uint32_t* __rest
         a2 = a3, a3 = t;
     }
     nd.axes[0] = a1, nd.axes[1] = a2, nd.axes[2] = a3;
-    nd.found = nd.count < 2 ? 2 : 0;  // single triangles never split (and never move)
+    // single triangles never split (and never move); small nodes finish in k_small_subtrees
+    nd.found = nd.count < 2 ? 2 : (nd.count <= small ? 3 : 0);
     nd.left = -1;
 }
 
@@ -327,6 +333,122 @@ __global__ void k_children(BNode* __restrict__ nodes, const uint32_t* __restrict
     next[s] = l, next[s + 1] = l + 1;
 }
 
+// ---------------------------------------------------------------------------------------
+// small nodes: BVH::Subdivide literally, one thread per subtree (its element range is its own).
+// Children come from a block of 2 (count - 1) node slots; `inner` is set for every node of the
+// subtree (post-order), the numbering pass below walks it top-down.
+// ---------------------------------------------------------------------------------------
+__device__ void small_bounds(BNode& nd, const float4* __restrict__ e, const GPUVertex* __restrict__ v,
+                             const GPUFace* __restrict__ f) {
+    for (int d = 0; d < 3; d++) nd.bmin[d] = 1e30f, nd.bmax[d] = -1e30f;
+    for (uint32_t y = 0; y < nd.count; y++) {
+        const uint32_t fi = __float_as_uint(e[nd.first + y].w);
+        const uint32_t vi[3] = {f[fi].v0, f[fi].v1, f[fi].v2};
+        for (uint32_t q : vi)
+            for (int d = 0; d < 3; d++) {
+                const float c = v[q].position[d];
+                nd.bmin[d] = rtm::gmin(nd.bmin[d], c);
+                nd.bmax[d] = rtm::gmax(nd.bmax[d], c);
+            }
+    }
+}
+
+__global__ void k_small_subtrees(BNode* __restrict__ nodes, const uint32_t* __restrict__ lvl, uint32_t nl,
+                                 float4* __restrict__ e, const GPUVertex* __restrict__ v,
+                                 const GPUFace* __restrict__ f, uint32_t* __restrict__ counters, int level) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nl) return;
+    const uint32_t root = lvl[i];
+    if (nodes[root].found != 3) return;
+    uint32_t next = atomicAdd(&counters[0], 2u * (nodes[root].count - 1u));
+    const uint32_t block_end = next + 2u * (nodes[root].count - 1u);
+    uint32_t stack[2 * SMALL];
+    int depth_of[2 * SMALL];
+    uint32_t order[2 * SMALL];  // pre-order of the subtree, for the post-order inner counts
+    uint32_t sp = 0, no = 0;
+    int maxd = level;
+    stack[sp] = root, depth_of[sp++] = level;
+    while (sp) {
+        sp--;
+        const uint32_t k = stack[sp];
+        const int dk = depth_of[sp];
+        maxd = max(maxd, dk);
+        order[no++] = k;
+        BNode& nd = nodes[k];
+        nd.left = -1;
+        if (nd.count < 2) continue;
+        const float ext[3] = {nd.bmax[0] - nd.bmin[0], nd.bmax[1] - nd.bmin[1], nd.bmax[2] - nd.bmin[2]};
+        int a1 = 0;
+        if (ext[1] > ext[0]) a1 = 1;
+        if (ext[2] > ext[a1]) a1 = 2;
+        int a2 = (a1 + 1) % 3, a3 = (a2 + 1) % 3;
+        if (ext[a3] > ext[a2]) {
+            const int t = a2;
+            a2 = a3, a3 = t;
+        }
+        const int axes[3] = {a1, a2, a3};
+        bool found = false;
+        int ii = 0, left_count = 0;
+        for (int q = 0; q < 3 && !found; q++) {
+            const int ax = axes[q];
+            const float split = nd.bmin[ax] + ext[ax] * 0.5f;
+            ii = (int)nd.first;
+            int jj = ii + (int)nd.count - 1;
+            while (ii <= jj) {
+                if (comp(e[ii], ax) < split) {
+                    ii++;
+                } else {
+                    const float4 t = e[ii];
+                    e[ii] = e[jj];
+                    e[jj--] = t;
+                }
+            }
+            left_count = ii - (int)nd.first;
+            found = left_count != 0 && left_count != (int)nd.count;
+        }
+        if (!found) continue;
+        const uint32_t l = next;
+        next += 2;
+        nd.left = (int32_t)l;
+        BNode& a = nodes[l];
+        BNode& b = nodes[l + 1];
+        a.first = nd.first, a.count = (uint32_t)left_count;
+        b.first = (uint32_t)ii, b.count = nd.count - (uint32_t)left_count;
+        small_bounds(a, e, v, f);
+        small_bounds(b, e, v, f);
+        stack[sp] = l + 1, depth_of[sp++] = dk + 1;  // left popped first (pre-order)
+        stack[sp] = l, depth_of[sp++] = dk + 1;
+    }
+    for (uint32_t u = next; u < block_end; u++) nodes[u].final_index = ~0u;  // unused slots
+    for (uint32_t q = no; q-- > 0;) {  // reverse pre-order: children before parents
+        BNode& nd = nodes[order[q]];
+        nd.inner = nd.left < 0 ? 0u : 1u + nodes[nd.left].inner + nodes[nd.left + 1].inner;
+    }
+    atomicMax(&counters[2], (uint32_t)maxd);
+}
+
+__global__ void k_small_number(BNode* __restrict__ nodes, const uint32_t* __restrict__ lvl, uint32_t nl) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nl) return;
+    const uint32_t root = lvl[i];
+    if (nodes[root].found != 3) return;
+    uint32_t stack[2 * SMALL];
+    uint32_t sp = 0;
+    stack[sp++] = root;
+    while (sp) {
+        const BNode& nd = nodes[stack[--sp]];
+        if (nd.left < 0) continue;
+        BNode& a = nodes[nd.left];
+        BNode& b = nodes[nd.left + 1];
+        const uint32_t c = 1u + 2u * nd.before;
+        a.final_index = c, b.final_index = c + 1;
+        a.before = nd.before + 1u;
+        b.before = a.before + a.inner;
+        stack[sp++] = nd.left + 1;
+        stack[sp++] = nd.left;
+    }
+}
+
 // numbering: inner-node counts bottom-up, pre-order ranks top-down
 __global__ void k_inner_up(BNode* __restrict__ nodes, const uint32_t* __restrict__ lvl, uint32_t nl) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -352,6 +474,7 @@ __global__ void k_emit(const BNode* __restrict__ nodes, uint32_t count, GPUBVHNo
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
     const BNode& nd = nodes[i];
+    if (nd.final_index == ~0u) return;  // a small subtree's unused slot
     GPUBVHNode o;
     for (int d = 0; d < 3; d++) o.bmin[d] = nd.bmin[d], o.bmax[d] = nd.bmax[d];
     if (nd.left >= 0) {
@@ -396,6 +519,11 @@ extern "C" int rt_bvh_build_device(const GPUVertex* vertices, uint32_t vertex_co
                                    uint32_t face_count, GPUBVHNode* nodes_out, uint32_t* face_indices_out,
                                    uint32_t* node_count_out, int* max_depth_out, void* stream) {
     hipStream_t st = (hipStream_t)stream;
+    static const uint32_t small = [] {
+        const char* e = std::getenv("RT_BVH_SMALL");  // tuning knob, <= SMALL
+        const uint32_t v = e ? (uint32_t)std::strtoul(e, nullptr, 0) : 16u;
+        return v < 2u ? 2u : (v > SMALL ? SMALL : v);
+    }();
     if (!vertices || !faces || !nodes_out || !face_indices_out || face_count == 0)
         return fail("rt_bvh_build_device: bad arguments");
     const uint32_t n = face_count;
@@ -425,8 +553,8 @@ extern "C" int rt_bvh_build_device(const GPUVertex* vertices, uint32_t vertex_co
     hipMemcpyAsync(nodes, &root, sizeof(BNode), hipMemcpyHostToDevice, st);
     const uint32_t zero_lvl = 0;
     hipMemcpyAsync(lvlbuf, &zero_lvl, 4, hipMemcpyHostToDevice, st);
-    uint32_t cnt[2] = {1, 0};  // nodes allocated, next-level size
-    hipMemcpyAsync(counters, cnt, 8, hipMemcpyHostToDevice, st);
+    uint32_t cnt[3] = {1, 0, 0};  // nodes allocated, next-level size, deepest small-subtree node
+    hipMemcpyAsync(counters, cnt, 12, hipMemcpyHostToDevice, st);
 
     // temp storage for the tile scan
     size_t scan_bytes = 0;
@@ -448,7 +576,7 @@ extern "C" int rt_bvh_build_device(const GPUVertex* vertices, uint32_t vertex_co
         const uint32_t total = last[0] + last[1];
         hipLaunchKernelGGL(k_bounds_tiles, dim3(total), dim3(TS), 0, st, nodes, lvl, nl, tile_start, total, e, vertices,
                            faces, part);
-        hipLaunchKernelGGL(k_bounds_nodes, dim3(blocks(nl)), dim3(256), 0, st, nodes, lvl, nl, tile_start, part);
+        hipLaunchKernelGGL(k_bounds_nodes, dim3(blocks(nl)), dim3(256), 0, st, nodes, lvl, nl, tile_start, part, small);
         for (int attempt = 0; attempt < 3; attempt++) {
             hipLaunchKernelGGL(k_split_pos, dim3(blocks(nl)), dim3(256), 0, st, nodes, lvl, nl, attempt);
             hipLaunchKernelGGL(k_count_left, dim3(total), dim3(TS), 0, st, nodes, lvl, nl, tile_start, total, e, attempt,
@@ -462,6 +590,8 @@ extern "C" int rt_bvh_build_device(const GPUVertex* vertices, uint32_t vertex_co
             hipLaunchKernelGGL(k_copy_back, dim3(total), dim3(TS), 0, st, nodes, lvl, nl, tile_start, total, tmp, e);
             hipLaunchKernelGGL(k_mark_found, dim3(blocks(nl)), dim3(256), 0, st, nodes, lvl, nl);
         }
+        hipLaunchKernelGGL(k_small_subtrees, dim3(blocks(nl, 64)), dim3(64), 0, st, nodes, lvl, nl, e, vertices, faces,
+                           counters, depth);
         const uint32_t next_off = off + nl;
         hipMemsetAsync(counters + 1, 0, 4, st);
         hipLaunchKernelGGL(k_children, dim3(blocks(nl)), dim3(256), 0, st, nodes, lvl, nl, counters, lvlbuf + next_off);
@@ -479,8 +609,9 @@ extern "C" int rt_bvh_build_device(const GPUVertex* vertices, uint32_t vertex_co
     }
     int badv = 0;
     hipMemcpyAsync(&badv, bad, sizeof(int), hipMemcpyDeviceToHost, st);
-    uint32_t total_nodes = 0;
+    uint32_t total_nodes = 0, small_depth = 0;
     hipMemcpyAsync(&total_nodes, counters, 4, hipMemcpyDeviceToHost, st);
+    hipMemcpyAsync(&small_depth, counters + 2, 4, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return fail("rt_bvh_build_device: sync failed");
     if (badv) return fail("rt_bvh_build_device: non-finite vertex positions (use the host builder)");
     // numbering: bottom-up inner counts, top-down pre-order ranks
@@ -490,11 +621,16 @@ extern "C" int rt_bvh_build_device(const GPUVertex* vertices, uint32_t vertex_co
     for (size_t L = 0; L < level_off.size(); L++)
         hipLaunchKernelGGL(k_rank_down, dim3(blocks(level_n[L])), dim3(256), 0, st, nodes, lvlbuf + level_off[L],
                            level_n[L]);
+    for (size_t L = 0; L < level_off.size(); L++)
+        hipLaunchKernelGGL(k_small_number, dim3(blocks(level_n[L], 64)), dim3(64), 0, st, nodes, lvlbuf + level_off[L],
+                           level_n[L]);
     hipLaunchKernelGGL(k_emit, dim3(blocks(total_nodes)), dim3(256), 0, st, nodes, total_nodes, nodes_out);
+    uint32_t root_inner = 0;
+    hipMemcpyAsync(&root_inner, &nodes[0].inner, 4, hipMemcpyDeviceToHost, st);
     hipLaunchKernelGGL(k_indices, dim3(blocks(n)), dim3(256), 0, st, e, n, face_indices_out);
     if (hipStreamSynchronize(st) != hipSuccess || hipGetLastError() != hipSuccess)
         return fail("rt_bvh_build_device: numbering failed");
-    if (node_count_out) *node_count_out = total_nodes;
-    if (max_depth_out) *max_depth_out = depth;
+    if (node_count_out) *node_count_out = 1u + 2u * root_inner;  // nodes_used
+    if (max_depth_out) *max_depth_out = depth > (int)small_depth ? depth : (int)small_depth;
     return 0;
 }

@@ -107,6 +107,7 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
             }();
             po = rt_build_leaf_tree(&out->tris[(size_t)nd.first_index * 12], nd.prim_count, prm, out->tree, out->ltris);
             rt_build_leaf_flat(out->tree, po, prm, out->flat);
+            if (out->ltris.size() / 12 >= (1u << 28)) bad("leaf trees too large (record index >= 2^28)");
             pf = 2;
             std::memcpy(&lead[10], &po, 4);
             std::memcpy(&lead[11], &pf, 4);

@@ -709,14 +709,14 @@ __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree
                 // surviving clusters, compacted in order through the wave's LDS scratch
                 if (need2) {
                     const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(mc >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mc, 0u));
-                    scratch[rk] = tb, scratch[64 + rk] = n;
+                    scratch[rk] = tb | (n << 28);  // n <= 8; leaf-tree records < 2^28
                 }
                 __builtin_amdgcn_wave_barrier();
                 for (uint32_t base = 0; base < nsc; base += 8u) {
                     if (TIMING && lane == 0) c.w_big++;
                     const uint32_t slot = base + (lane >> 3), i = lane & 7u;
                     if (slot < nsc) {
-                        const uint32_t my_tb = scratch[slot], my_n = scratch[64 + slot];
+                        const uint32_t w = scratch[slot], my_tb = w & 0x0fffffffu, my_n = w >> 28;
                         if (i < my_n) {
                             const size_t t3 = 3 * (size_t)(my_tb + i);
                             leaf_candidate(B, ltris[t3], ltris[t3 + 1], ltris[t3 + 2], L);

@@ -675,19 +675,19 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
 template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
     __shared__ uint32_t stack_lds[STACK * WAVE];  // one word per entry (rt_fast.h pop)
-    __shared__ uint32_t scratch_lds[(MODE & 4) ? 128 : 1];  // coop_tree's cluster compaction
+    __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
     render_fast_body<STACK, STATS, MODE>(a, stack_lds + threadIdx.x, scratch_lds);
 }
 template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(5))) void render_fast_kernel_w5(RenderArgs a) {
     __shared__ uint32_t stack_lds[STACK * WAVE];
-    __shared__ uint32_t scratch_lds[(MODE & 4) ? 128 : 1];  // coop_tree's cluster compaction
+    __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
     render_fast_body<STACK, STATS, MODE>(a, stack_lds + threadIdx.x, scratch_lds);
 }
 template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(6))) void render_fast_kernel_w6(RenderArgs a) {
     __shared__ uint32_t stack_lds[STACK * WAVE];
-    __shared__ uint32_t scratch_lds[(MODE & 4) ? 128 : 1];  // coop_tree's cluster compaction
+    __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
     render_fast_body<STACK, STATS, MODE>(a, stack_lds + threadIdx.x, scratch_lds);
 }
 
@@ -815,8 +815,10 @@ hipError_t launch_fast_t(const RenderArgs& args, int tiles, hipStream_t stream) 
 }
 
 hipError_t launch_fast(const RenderArgs& args, int tiles, int depth, bool stats, hipStream_t s) {
-    if (depth >= 0 && depth + 2 <= 28)
-        return stats ? launch_fast_t<28, true>(args, tiles, s) : launch_fast_t<28, false>(args, tiles, s);
+    // 30 entries: 7.5 KB of LDS per wave (+256 B scratch in tree scenes) still fits 5 waves per
+    // SIMD, and covers the 4-bunny scene's depth 28 (STACK 40 would leave it at 3 waves per SIMD)
+    if (depth >= 0 && depth + 2 <= 30)
+        return stats ? launch_fast_t<30, true>(args, tiles, s) : launch_fast_t<30, false>(args, tiles, s);
     if (depth >= 0 && depth + 2 <= 40)
         return stats ? launch_fast_t<40, true>(args, tiles, s) : launch_fast_t<40, false>(args, tiles, s);
     return stats ? launch_fast_t<64, true>(args, tiles, s) : launch_fast_t<64, false>(args, tiles, s);
