@@ -127,6 +127,26 @@ def check_unsharded(rt, scene_name, W, H, spp, bounces, frames, final):
     return bool(torch.equal(a, rt.surface_view(final, W).contiguous().view(torch.int32)))
 
 
+def load_issue(cfg):
+    """The render kernel's issue-side counters from the committed PMC summary: the path is
+    VALU-issue bound (the scene lives in L2 / Infinity Cache), so the HBM fraction alone does not
+    say how close the kernel is to its limit."""
+    out = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(path))
+            c = d["kernels"][d["kernel"]]["counters"]
+        except Exception:
+            continue
+        if d.get("config") == cfg:
+            out = {"bound": "valu", "valu_busy": round(c["VALUBusy"] / 100.0, 3),
+                   "lane_utilization": round(c["VALUUtilization"] / 100.0, 3),
+                   "valu_wave_instructions_per_launch": int(c["SQ_INSTS_VALU"]),
+                   "l2_hit_rate": round(d.get("l2_hit_rate", 0.0), 3),
+                   "source": os.path.relpath(path, ROOT)}
+    return out
+
+
 def load_traffic(cfg):
     """HBM bytes per render launch from a committed PMC summary (profiles/*pmc*.json), if any."""
     best = None
@@ -296,6 +316,7 @@ def main():
                        "segments_per_step": round(segs_total / args.steps, 1)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config),
+                         "issue": load_issue(args.config),
                          "kernel": "render_fast_kernel", "kernel_ms": round(kern_avg_s * 1e3, 3),
                          "algorithmic_bytes_per_launch": int(bytes_per_launch),
                          "frame0_counts": {k: int(v) for k, v in zip(rt.STAT_NAMES, stats0) if k}},
