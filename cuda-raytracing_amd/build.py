@@ -52,18 +52,22 @@ def build_product(force=False):
     deps = _deps(CSRC, (".h", ".hip", ".cpp")) + _deps(INC, (".h",)) + [os.path.abspath(__file__)]
     if not force and _newer(LIB, deps):
         return LIB
-    objs = []
+    jobs = []
     for src in HIP_SOURCES:
         obj = os.path.join(BUILD, src + ".o")
-        _run([HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *FP_FLAGS,
-              "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics", "-fno-slp-vectorize", "-I", INC, "-I", CSRC,
-              "-c", os.path.join(CSRC, src), "-o", obj])
-        objs.append(obj)
+        jobs.append((obj, [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *FP_FLAGS,
+                           "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics", "-fno-slp-vectorize",
+                           "-I", INC, "-I", CSRC, "-c", os.path.join(CSRC, src), "-o", obj]))
     for src in HOST_SOURCES:
         obj = os.path.join(BUILD, src + ".o")
-        _run(["g++", "-O2", "-std=c++17", "-fPIC", *FP_FLAGS, "-I", INC, "-I", CSRC,
-              "-c", os.path.join(CSRC, src), "-o", obj])
-        objs.append(obj)
+        jobs.append((obj, ["g++", "-O2", "-std=c++17", "-fPIC", *FP_FLAGS, "-I", INC, "-I", CSRC,
+                           "-c", os.path.join(CSRC, src), "-o", obj]))
+    # translation units compile in parallel (the render kernel's dominates)
+    from concurrent.futures import ThreadPoolExecutor
+    workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 8))
+    with ThreadPoolExecutor(max_workers=workers) as ex:
+        list(ex.map(lambda j: _run(j[1]), jobs))
+    objs = [o for o, _ in jobs]
     tmp = LIB + ".tmp"
     _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp])
     os.replace(tmp, LIB)
