@@ -57,7 +57,7 @@ struct Counters {
     unsigned long long w_small = 0, l_small = 0, w_big = 0, l_big = 0, w_seg = 0, l_seg = 0;
     unsigned long long ktest = 0, ktri = 0;  // leaf-tree node visits / triangle tests
     unsigned long long cy_small = 0, cy_big = 0, r_coop = 0, r_shared = 0, coop_rays = 0, w_iter = 0;  // timing
-    unsigned long long cy_tcl = 0, cy_ttri = 0;  // timing: leaf-tree cluster / triangle rounds
+    unsigned long long cy_tcl = 0, cy_ttri = 0, cy_tree = 0;  // timing: leaf-tree cluster / triangle rounds, whole walk
 };
 
 __device__ __forceinline__ rtm::f3 ld3(const float* p) { return rtm::f3{p[0], p[1], p[2]}; }

@@ -620,6 +620,13 @@ struct Trav {
 // and the wave's (t, position) arg-min is exactly the sequential loop's result.  A NaN distance
 // sends the ray to the sequential loop.  The per-lane walk (tree_leaf) runs each lane's ray on
 // one lane, at a few percent lane utilisation; here all 64 lanes work on one ray.
+// device-library wave reduction (DPP), over the active lanes
+extern "C" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);
+
+// Order-preserving key of a distance t >= 0 (found candidates only): +-0 share key 0, so a tie
+// between them is decided by position, as the float comparison `t == best` does.
+__device__ __forceinline__ uint32_t tkey(float t) { return t == 0.0f ? 0u : __float_as_uint(t); }
+
 __device__ __forceinline__ f3 bcast3(f3 v, int lane) {
     return rtm::mk(bcast(v.x, lane), bcast(v.y, lane), bcast(v.z, lane));
 }
@@ -728,10 +735,8 @@ __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree
                 // tighten the cull bound to just above the best candidate so far (ties on t are
                 // decided by position, so a triangle at exactly that distance must stay in)
                 if (__ballot(L.found)) {
-                    float mt = L.found ? L.t : __int_as_float(0x7f800000);
-                    for (int off = 32; off > 0; off >>= 1) mt = fminf(mt, __shfl_xor(mt, off));
-                    mt = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(mt)));
-                    const float up = __uint_as_float(__float_as_uint(mt) + 1u);  // mt >= 0, finite
+                    const uint32_t mk2 = __ockl_wfred_min_u32(L.found ? tkey(L.t) : 0xffffffffu);
+                    const float up = __uint_as_float(mk2 + 1u);  // next float above the best (>= 0, finite)
                     cbest = fminf(cbest, up);
                 }
             }
@@ -751,18 +756,10 @@ __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree
             }
             continue;
         }
-        // arg-min of (t, position) over the lanes holding a candidate
-        float mt = L.found ? L.t : __int_as_float(0x7f800000);
-        uint32_t mj = L.found ? L.j : 0xffffffffu;
-        for (int off = 32; off > 0; off >>= 1) {
-            const float ot = __shfl_xor(mt, off);
-            const uint32_t oj = (uint32_t)__shfl_xor((int)mj, off);
-            const bool take = ot < mt || (ot == mt && oj < mj);
-            mt = take ? ot : mt;
-            mj = take ? oj : mj;
-        }
-        mj = __builtin_amdgcn_readfirstlane(mj);
-        if (mj != 0xffffffffu) {
+        // arg-min of (t, position) over the lanes holding a candidate: smallest t, then position
+        const uint32_t mt = __ockl_wfred_min_u32(L.found ? tkey(L.t) : 0xffffffffu);
+        const uint32_t mj = __ockl_wfred_min_u32(L.found && tkey(L.t) == mt ? L.j : 0xffffffffu);
+        if (mt != 0xffffffffu) {
             const int wl = __ffsll((long long)__ballot(L.found && L.j == mj)) - 1;
             const float wt = bcast(L.t, wl), wbx = bcast(L.bx, wl), wby = bcast(L.by, wl);
             const uint32_t wid = (uint32_t)__builtin_amdgcn_readlane((int)L.id, wl);
@@ -826,7 +823,11 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
         const unsigned long long mt = __ballot(at_tree);
         if (mt) {
             if (!STATS && flat && (tune & 8192u) == 0)  // RT_TUNE bit 13: per-lane walk instead
+            {
+                const unsigned long long tt0 = (MODE & 8) ? __builtin_amdgcn_s_memtime() : 0;
                 coop_tree<(MODE & 8) != 0>(tris, tree, ltris, flat, mt, root, R, h, T, scratch, c);
+                if (MODE & 8) c.cy_tree += __builtin_amdgcn_s_memtime() - tt0;
+            }
             else if (at_tree)
                 tree_leaf<STATS>(tris, tree, ltris, root, T.first, T.count, R, h, c);
             return at_tree;

@@ -634,6 +634,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
         atomicAdd(a.stats + RT_STAT_WAVE_BIG_TRIS, c.w_big);
         atomicAdd(a.stats + RT_STAT_LANE_BIG_TRIS, c.l_big);
         atomicAdd(a.stats + RT_STAT_CYCLES_TREE_CLUSTERS, c.cy_tcl);
+        atomicAdd(a.stats + RT_STAT_CYCLES_TREE_CUT, c.cy_tree);
         atomicAdd(a.stats + RT_STAT_CYCLES_TREE_TRIS, c.cy_ttri);
         // RT_TUNE bit 11: per-wave clocks (start, end) after the counters, for load-balance analysis
         if (a.tune & 2048u) {
@@ -661,6 +662,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
         atomicAdd(a.stats + RT_STAT_WAVE_BIG_TRIS, c.w_big);
         atomicAdd(a.stats + RT_STAT_LANE_BIG_TRIS, c.l_big);
         atomicAdd(a.stats + RT_STAT_CYCLES_TREE_CLUSTERS, c.cy_tcl);
+        atomicAdd(a.stats + RT_STAT_CYCLES_TREE_CUT, c.cy_tree);
         atomicAdd(a.stats + RT_STAT_CYCLES_TREE_TRIS, c.cy_ttri);
         atomicAdd(a.stats + RT_STAT_WAVE_SEGMENT_ITERS, c.w_seg);
         atomicAdd(a.stats + RT_STAT_LANE_SEGMENTS, c.l_seg);

@@ -195,7 +195,7 @@ enum {
     RT_STAT_ROUNDS_COOP = 19,       /* cooperative big-leaf rounds */
     RT_STAT_ROUNDS_SHARED = 20,     /* shared-leaf (pair / scalar-load) rounds */
     RT_STAT_COOP_RAYS = 21,         /* rays run through cooperative rounds */
-    RT_STAT_CYCLES_TREE_CUT = 7,    /* timing frames, cooperative leaf-tree walk: set-up, subtree screen, reduction */
+    RT_STAT_CYCLES_TREE_CUT = 7,    /* timing frames, cooperative leaf-tree walk: whole walk (all rounds) */
     RT_STAT_CYCLES_TREE_CLUSTERS = 22, /* ... cluster screening rounds */
     RT_STAT_CYCLES_TREE_TRIS = 23,  /* ... triangle rounds */
     RT_STAT_COUNT = 24
