@@ -345,6 +345,13 @@ __device__ __forceinline__ void pair_test(const Ray& R, const Pair& P, Hit& h) {
     }
 }
 
+// device-library wave reduction (DPP), over the active lanes
+extern "C" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);
+
+// Order-preserving key of a distance t >= 0 (found candidates only): +-0 share key 0, so a tie
+// between them is decided by position, as the float comparison `t == best` does.
+__device__ __forceinline__ uint32_t tkey(float t) { return t == 0.0f ? 0u : __float_as_uint(t); }
+
 __device__ __forceinline__ float bcast(float v, int lane) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
@@ -399,17 +406,10 @@ __device__ __forceinline__ void coop_leaf(const float4* tris, const float4* pair
             }
             continue;
         }
-        // arg-min of (t, index) across the wave
-        float mt = bt;
-        uint32_t mi = bi;
-        for (int off = 32; off > 0; off >>= 1) {
-            const float ot = __shfl_xor(mt, off);
-            const uint32_t oi = (uint32_t)__shfl_xor((int)mi, off);
-            const bool take = ot < mt || (ot == mt && oi < mi);
-            mt = take ? ot : mt;
-            mi = take ? oi : mi;
-        }
-        mi = __builtin_amdgcn_readfirstlane(mi);
+        // arg-min of (t, index) across the wave (DPP wave reductions)
+        const bool has = bi != 0xffffffffu;
+        const uint32_t mk = __ockl_wfred_min_u32(has ? tkey(bt) : 0xffffffffu);
+        const uint32_t mi = __ockl_wfred_min_u32(has && tkey(bt) == mk ? bi : 0xffffffffu);
         if (mi != 0xffffffffu) {
             const int wl = (int)((mi >> 1) & 63u);  // lane that tested pair mi / 2
             const float wbx = bcast(bx, wl), wby = bcast(by, wl), wt = bcast(bt, wl);
@@ -451,16 +451,10 @@ __device__ __forceinline__ void coop_leaf_scalar(const float4* tris, unsigned lo
             }
             continue;
         }
-        float mt = bt;
-        uint32_t mi = bi;
-        for (int off = 32; off > 0; off >>= 1) {
-            const float ot = __shfl_xor(mt, off);
-            const uint32_t oi = (uint32_t)__shfl_xor((int)mi, off);
-            const bool take = ot < mt || (ot == mt && oi < mi);
-            mt = take ? ot : mt;
-            mi = take ? oi : mi;
-        }
-        mi = __builtin_amdgcn_readfirstlane(mi);
+        // (t, index) arg-min over the lanes holding a candidate (DPP wave reductions)
+        const bool has = bi != 0xffffffffu;
+        const uint32_t mk = __ockl_wfred_min_u32(has ? tkey(bt) : 0xffffffffu);
+        const uint32_t mi = __ockl_wfred_min_u32(has && tkey(bt) == mk ? bi : 0xffffffffu);
         if (mi != 0xffffffffu) {
             const int wl = (int)(mi & 63u);
             const float wbx = bcast(bx, wl), wby = bcast(by, wl), wt = bcast(bt, wl);
@@ -620,13 +614,6 @@ struct Trav {
 // and the wave's (t, position) arg-min is exactly the sequential loop's result.  A NaN distance
 // sends the ray to the sequential loop.  The per-lane walk (tree_leaf) runs each lane's ray on
 // one lane, at a few percent lane utilisation; here all 64 lanes work on one ray.
-// device-library wave reduction (DPP), over the active lanes
-extern "C" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);
-
-// Order-preserving key of a distance t >= 0 (found candidates only): +-0 share key 0, so a tie
-// between them is decided by position, as the float comparison `t == best` does.
-__device__ __forceinline__ uint32_t tkey(float t) { return t == 0.0f ? 0u : __float_as_uint(t); }
-
 __device__ __forceinline__ f3 bcast3(f3 v, int lane) {
     return rtm::mk(bcast(v.x, lane), bcast(v.y, lane), bcast(v.z, lane));
 }
