@@ -607,8 +607,8 @@ struct Trav {
 
 // Cooperative walk of the leaf trees through their flat lists (leaftree.h) for the lanes `m`
 // waiting at tree leaves, one ray at a time: the whole wave screens the cut subtrees (a lane per
-// subtree), then -- nearest box first -- the clusters of the surviving subtrees (a lane per
-// cluster, two subtrees per round), then the triangles of the surviving clusters (8 lanes per
+// subtree), then the clusters of the surviving subtrees (a lane per cluster, two subtrees per
+// round), then the triangles of the surviving clusters (8 lanes per
 // cluster, 8 clusters per round); the cull bound drops to the best candidate found so far.  cluster_cull excludes only what provably cannot pass the fp32 test with
 // 0 <= t < best; every lane keeps the (t, position) minimum of what it tested (leaf_candidate),
 // and the wave's (t, position) arg-min is exactly the sequential loop's result.  A NaN distance
@@ -621,8 +621,11 @@ __device__ __forceinline__ f3 bcast3(f3 v, int lane) {
 template <bool TIMING, class C>
 __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree, const float4* ltris, const float4* flat,
                                           unsigned long long m, uint32_t root_l, const Ray& R, Hit& h, const Trav& T,
-                                          uint32_t* scratch, C& c) {
+                                          uint32_t* scratch, uint32_t tune, C& c) {
     const uint32_t lane = threadIdx.x & 63u;
+    // RT_TUNE bit 14: visit surviving subtrees nearest box first (costs more than it saves here:
+    // 117 vs 111 ms on the 4-bunny frame), else in tree order
+    const bool order = (tune & 16384u) != 0;
     const f3 rnd_l = rtm::mk(1.0f / R.nd.x, 1.0f / R.nd.y, 1.0f / R.nd.z);  // cluster_cull's reciprocals
     while (m) {
         const int r = __ffsll((long long)m) - 1;
@@ -656,22 +659,27 @@ __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree
                 const float4 K0 = ct[4 * k], K1 = ct[4 * k + 1], K3 = ct[4 * k + 3];
                 s0 = __float_as_uint(K3.y), s1 = __float_as_uint(K3.z);
                 need = !(cull_ok && (__float_as_uint(K3.w) & 1u) && cluster_cull(B, rnd, cbest, K0, K1, ct[4 * k + 2], K3));
-                // box entry distance along the ray, only to visit near subtrees first
-                const float tx1 = (K0.x - B.o.x) * rnd.x, tx2 = (K1.x - B.o.x) * rnd.x;
-                const float ty1 = (K0.y - B.o.y) * rnd.y, ty2 = (K1.y - B.o.y) * rnd.y;
-                const float tz1 = (K0.z - B.o.z) * rnd.z, tz2 = (K1.z - B.o.z) * rnd.z;
-                te = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
-                te = te == te ? te : 0.0f;
+                if (order) {  // box entry distance along the ray, only to order the subtrees
+                    const float tx1 = (K0.x - B.o.x) * rnd.x, tx2 = (K1.x - B.o.x) * rnd.x;
+                    const float ty1 = (K0.y - B.o.y) * rnd.y, ty2 = (K1.y - B.o.y) * rnd.y;
+                    const float tz1 = (K0.z - B.o.z) * rnd.z, tz2 = (K1.z - B.o.z) * rnd.z;
+                    te = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+                    te = te == te ? te : 0.0f;
+                }
             }
             const unsigned long long mk = __ballot(need);
             const uint32_t ns = (uint32_t)__popcll(mk);
             if (TIMING && lane == 0) c.ktest += min(64u, nk - kbase), c.r_shared += ns;
             // near-first order of the surviving subtrees: rank by (entry distance, lane)
             uint32_t rank = 0;
-            for (unsigned long long w = mk; w; w &= w - 1) {
-                const int b = __ffsll((long long)w) - 1;
-                const float tb = bcast(te, b);
-                rank += (tb < te || (tb == te && b < (int)lane)) ? 1u : 0u;
+            if (order) {
+                for (unsigned long long w = mk; w; w &= w - 1) {
+                    const int b = __ffsll((long long)w) - 1;
+                    const float tb = bcast(te, b);
+                    rank += (tb < te || (tb == te && b < (int)lane)) ? 1u : 0u;
+                }
+            } else {
+                rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
             }
             for (uint32_t q = 0; q < ns; q += 2) {
                 // two subtrees per round (<= 32 clusters each): lanes 0-31 and 32-63
@@ -812,7 +820,7 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
             if (!STATS && flat && (tune & 8192u) == 0)  // RT_TUNE bit 13: per-lane walk instead
             {
                 const unsigned long long tt0 = (MODE & 8) ? __builtin_amdgcn_s_memtime() : 0;
-                coop_tree<(MODE & 8) != 0>(tris, tree, ltris, flat, mt, root, R, h, T, scratch, c);
+                coop_tree<(MODE & 8) != 0>(tris, tree, ltris, flat, mt, root, R, h, T, scratch, tune, c);
                 if (MODE & 8) c.cy_tree += __builtin_amdgcn_s_memtime() - tt0;
             }
             else if (at_tree)
