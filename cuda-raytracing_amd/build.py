@@ -74,6 +74,22 @@ def build_product(force=False):
     return LIB
 
 
+HOST_DRIVER_SRC = os.path.join(ROOT, "tests", "cpp", "host_driver.cpp")
+HOST_DRIVER = os.path.join(ROOT, "tests", "cpp", "host_driver")
+
+
+def build_host_driver(force=False):
+    """The C++ host of tests/test_cpp_host.py: drives librt_hip.so through include/rt_abi.h."""
+    deps = [HOST_DRIVER_SRC, LIB, os.path.join(INC, "rt_abi.h")]
+    if not os.path.exists(HOST_DRIVER_SRC) or (not force and _newer(HOST_DRIVER, deps)):
+        return HOST_DRIVER
+    tmp = HOST_DRIVER + ".tmp"
+    _run(["g++", "-O2", "-std=c++17", "-I", INC, HOST_DRIVER_SRC, "-L", PKG, "-lrt_hip",
+          "-Wl,-rpath,$ORIGIN/../../cuda-raytracing_amd", "-o", tmp])
+    os.replace(tmp, HOST_DRIVER)
+    return HOST_DRIVER
+
+
 def build_oracle(force=False):
     src = os.path.join(ORACLE_DIR, "rt_oracle.c")
     deps = [src, os.path.abspath(__file__)] + _deps(ORACLE_DIR, (".h",))
@@ -88,6 +104,7 @@ def build_oracle(force=False):
 def build_all(force=False):
     build_product(force)
     build_oracle(force)
+    build_host_driver(force)
 
 
 if __name__ == "__main__":
