@@ -121,3 +121,23 @@ def test_gpu_bvh_random_soups(seed):
         s.add_triangle(t[0], t[1], t[2], 0)
     s.build()
     _gpu_vs_host(rt, s)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,kind", [(1, "random"), (2, "random"), (3, "random"), (17, "identical"),
+                                    (40, "random"), (300, "collinear")])
+def test_gpu_bvh_tiny_and_degenerate(n, kind):
+    """One triangle, a handful, all identical (nothing splits: one leaf), and centroids on one line."""
+    rt = T.load_rt()
+    g = np.random.default_rng(n)
+    s = rt.Scene()
+    s.add_material()
+    pts = g.normal(size=(n, 3, 3)).astype(np.float32)
+    if kind == "identical":
+        pts[:] = pts[0]
+    elif kind == "collinear":
+        pts[:, :, 1:] = np.float32(0.5)
+    for t in pts:
+        s.add_triangle(t[0], t[1], t[2], 0)
+    s.build()
+    _gpu_vs_host(rt, s)
