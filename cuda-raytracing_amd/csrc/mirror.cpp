@@ -102,12 +102,12 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
                 const char* e = std::getenv("RT_CUT_CLUSTERS");  // tuning knobs
                 if (e) p.cut_clusters = std::min<uint32_t>(32u, (uint32_t)std::strtoul(e, nullptr, 0));
                 if ((e = std::getenv("RT_SPLIT_ANGLE"))) p.split_angle = std::strtod(e, nullptr);
-                if ((e = std::getenv("RT_CLUSTER_MAX"))) p.cluster_max = std::min<uint32_t>(8u, (uint32_t)std::strtoul(e, nullptr, 0));
+                if ((e = std::getenv("RT_CLUSTER_MAX"))) p.cluster_max = std::min<uint32_t>(kClusterMax, (uint32_t)std::strtoul(e, nullptr, 0));
                 return p;
             }();
             po = rt_build_leaf_tree(&out->tris[(size_t)nd.first_index * 12], nd.prim_count, prm, out->tree, out->ltris);
             rt_build_leaf_flat(out->tree, po, prm, out->flat);
-            if (out->ltris.size() / 12 >= (1u << 28)) bad("leaf trees too large (record index >= 2^28)");
+            if (out->ltris.size() / 12 >= (1u << 26)) bad("leaf trees too large (record index >= 2^26)");
             pf = 2;
             std::memcpy(&lead[10], &po, 4);
             std::memcpy(&lead[11], &pf, 4);

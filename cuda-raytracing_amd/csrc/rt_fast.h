@@ -608,8 +608,7 @@ struct Trav {
 // Cooperative walk of the leaf trees through their flat lists (leaftree.h) for the lanes `m`
 // waiting at tree leaves, one ray at a time: the whole wave screens the cut subtrees (a lane per
 // subtree), then the clusters of the surviving subtrees (a lane per cluster, two subtrees per
-// round), then the triangles of the surviving clusters (8 lanes per
-// cluster, 8 clusters per round); the cull bound drops to the best candidate found so far.  cluster_cull excludes only what provably cannot pass the fp32 test with
+// round), then the triangles of the surviving clusters (kClusterMax lanes per cluster); the cull bound drops to the best candidate found so far.  cluster_cull excludes only what provably cannot pass the fp32 test with
 // 0 <= t < best; every lane keeps the (t, position) minimum of what it tested (leaf_candidate),
 // and the wave's (t, position) arg-min is exactly the sequential loop's result.  A NaN distance
 // sends the ray to the sequential loop.  The per-lane walk (tree_leaf) runs each lane's ray on
@@ -711,14 +710,15 @@ __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree
                 // surviving clusters, compacted in order through the wave's LDS scratch
                 if (need2) {
                     const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(mc >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mc, 0u));
-                    scratch[rk] = tb | (n << 28);  // n <= 8; leaf-tree records < 2^28
+                    scratch[rk] = tb | ((n - 1u) << 26);  // 1 <= n <= kClusterMax <= 64; records < 2^26
                 }
                 __builtin_amdgcn_wave_barrier();
-                for (uint32_t base = 0; base < nsc; base += 8u) {
+                constexpr uint32_t CL = kClusterMax, PER = 64u / kClusterMax;  // lanes per cluster, clusters per round
+                for (uint32_t base = 0; base < nsc; base += PER) {
                     if (TIMING && lane == 0) c.w_big++;
-                    const uint32_t slot = base + (lane >> 3), i = lane & 7u;
+                    const uint32_t slot = base + lane / CL, i = lane % CL;
                     if (slot < nsc) {
-                        const uint32_t w = scratch[slot], my_tb = w & 0x0fffffffu, my_n = w >> 28;
+                        const uint32_t w = scratch[slot], my_tb = w & 0x03ffffffu, my_n = (w >> 26) + 1u;
                         if (i < my_n) {
                             const size_t t3 = 3 * (size_t)(my_tb + i);
                             leaf_candidate(B, ltris[t3], ltris[t3 + 1], ltris[t3 + 2], L);

@@ -27,6 +27,7 @@
 #include "rt_math.h"
 #include "xorwow.h"
 #include "rt_common.h"
+#include "leaftree.h"
 #include "rt_fast.h"
 
 #include "mirror.h"
