@@ -622,9 +622,9 @@ __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree
                                           unsigned long long m, uint32_t root_l, const Ray& R, Hit& h, const Trav& T,
                                           uint32_t* scratch, uint32_t tune, C& c) {
     const uint32_t lane = threadIdx.x & 63u;
-    // RT_TUNE bit 14: visit surviving subtrees nearest box first (costs more than it saves here:
+    // RT_TUNE bit 31: visit surviving subtrees nearest box first (costs more than it saves here:
     // 117 vs 111 ms on the 4-bunny frame), else in tree order
-    const bool order = (tune & 16384u) != 0;
+    const bool order = (tune & 0x80000000u) != 0;
     const f3 rnd_l = rtm::mk(1.0f / R.nd.x, 1.0f / R.nd.y, 1.0f / R.nd.z);  // cluster_cull's reciprocals
     while (m) {
         const int r = __ffsll((long long)m) - 1;
@@ -817,7 +817,7 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
         }
         const unsigned long long mt = __ballot(at_tree);
         if (mt) {
-            if (!STATS && flat && (tune & 8192u) == 0)  // RT_TUNE bit 13: per-lane walk instead
+            if (!STATS && flat && (tune & 0x40000000u) == 0)  // RT_TUNE bit 30: per-lane walk instead
             {
                 const unsigned long long tt0 = (MODE & 8) ? __builtin_amdgcn_s_memtime() : 0;
                 coop_tree<(MODE & 8) != 0>(tris, tree, ltris, flat, mt, root, R, h, T, scratch, tune, c);
@@ -940,7 +940,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
             c.cy_small += t1 - t0;
             t0 = t1;
         }
-        const unsigned long long big = __ballot(active);
+        const unsigned long long big = __ballot(active);  // every active lane waits at a big leaf
         if (!big) break;
         if (big_round<STATS, MODE>(tris, pairs, tree, ltris, flat, scratch, tune, big, active, R, h, T, c))
             active = pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
