@@ -141,3 +141,24 @@ def test_gpu_bvh_tiny_and_degenerate(n, kind):
         s.add_triangle(t[0], t[1], t[2], 0)
     s.build()
     _gpu_vs_host(rt, s)
+
+
+@pytest.mark.gpu
+def test_gpu_bvh_rejects_non_finite():
+    """Non-finite positions make glm::min/max order-dependent: the GPU builder refuses them (the
+    scene upload then falls back to the host builder)."""
+    import torch
+    rt = T.load_rt()
+    s = rt.Scene()
+    s.add_material()
+    g = np.random.default_rng(7)
+    for t in g.normal(size=(8, 3, 3)).astype(np.float32):
+        s.add_triangle(t[0], t[1], t[2], 0)
+    s.build()
+    h = s.host_arrays()
+    vv = h["vertices"].view(np.float32).reshape(-1, 8).copy()
+    vv[3, 1] = np.nan
+    v = torch.from_numpy(vv).cuda()
+    f = torch.from_numpy(h["faces"].view(np.int32).reshape(-1, 4).copy()).cuda()
+    with pytest.raises(rt.RTError):
+        rt.bvh_build_device(v, f)
