@@ -519,16 +519,33 @@ __device__ __forceinline__ void leaf_candidate(const Ray& R, float4 A, float4 B,
 // the ray segment [-Et, min(best, Tmax) + Et] against the box grown by r, with a margin m
 // (2^-16 relative) that absorbs the rounding of the test itself.  Rays outside the filtered
 // range (R.fast false) are never culled.  tests/test_leaf_tree.py checks the bound on the host.
+// Upper bounds may come from the hardware's 1-ulp sqrt / reciprocal on the device: every use below
+// is followed by a (1 + 2^-20) widening, which covers their error (the host uses IEEE sqrt / divide).
+RT_HD float cull_sqrt(float x) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_sqrtf(x);
+#else
+    return sqrtf(x);
+#endif
+}
+RT_HD float cull_div(float a, float b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return a * __builtin_amdgcn_rcpf(b);
+#else
+    return a / b;
+#endif
+}
+
 RT_HD bool cluster_cull(const Ray& R, f3 rnd, float best, float4 K0, float4 K1, float4 K2, float4 K3) {
     const float U = 0x1p-24f;
     if (!(best == best)) return false;
     const float E1 = K0.w, Nmin = K1.w;
     const float dota = fabsf(R.nd.x * K2.x + R.nd.y * K2.y + R.nd.z * K2.z);
     const float ca = fminf(fmaxf(dota * (1.0f - 0x1p-20f) - 4.0f * U, 0.0f), 1.0f);  // <= cos(angle(nd, axis))
-    const float sa = sqrtf(fmaxf(1.0f - ca * ca, 0.0f) + 2.0f * U) * (1.0f + 0x1p-20f);  // >= its sine
+    const float sa = cull_sqrt(fmaxf(1.0f - ca * ca, 0.0f) + 2.0f * U) * (1.0f + 0x1p-20f);  // >= its sine
     const float dlb = Nmin * ((ca * K2.w - sa * K3.x) - 4.0f * U) * (1.0f - 0x1p-20f);  // <= min |det|
     if (!(dlb > 36.0f * U * E1 * E1)) return false;
-    const float g = E1 / dlb * (1.0f + 0x1p-20f);
+    const float g = cull_div(E1, dlb) * (1.0f + 0x1p-20f);
     const float dx = fmaxf(fabsf(R.o.x - K0.x), fabsf(R.o.x - K1.x));
     const float dy = fmaxf(fabsf(R.o.y - K0.y), fabsf(R.o.y - K1.y));
     const float dz = fmaxf(fabsf(R.o.z - K0.z), fabsf(R.o.z - K1.z));
