@@ -49,7 +49,8 @@ struct RenderArgs {
     const float4* spairs; // small leaves' triangles in packed pairs, pair (i, i+1) at record i, or null
     const float4* flat;   // leaf trees' flat cluster / cut lists (leaftree.h) or null
     uint32_t tune;  // A/B knobs (RT_TUNE, rt_render; see rt_fast.h / rt_kernel.hip for the rest: bits 12-15
-                    // split steps, 30 per-lane leaf-tree walk, 31 subtree order):
+                    // split steps, 16-19 XCD run length (rt_kernel.hip xcd_block), 30 per-lane leaf-tree
+                    // walk, 31 subtree order):
                     // bit0 no cooperative leaf rounds, bit1 no pair
                     // records, bit2 no leaf trees, bit3 no small-leaf pairs, bits 4-5 big-leaf mode (rt_kernel.hip launch_fast_t)
 };

@@ -489,6 +489,22 @@ __device__ __forceinline__ bool shade_segment(const RenderArgs& a, const rtfast:
     return end;
 }
 
+// Logical sub-tile of this workgroup.  The dispatcher deals workgroups round-robin over the 8
+// XCDs (workgroup g -> XCD g % 8), so consecutive sub-tiles would land in different L2s.
+// Instead XCD x takes runs of S = 2^v consecutive sub-tiles: its i-th workgroup renders
+// sub-tile ((i / S) * 8 + x) * S + i % S (a permutation of the first multiple of 8S workgroups;
+// the rest keep their index), so neighbouring pixels share an L2.  v = 5 (runs of 8 tiles,
+// 128x16 px): config 2 18.29 -> 17.73 ms; v = 4 17.8, v = 6 18.1, v = 1-3 18.1-18.3.
+// RT_TUNE bits 16-19 override v; 15 keeps the dispatcher's order.
+__device__ __forceinline__ int xcd_block(uint32_t tune) {
+    const uint32_t g = blockIdx.x, tv = (tune >> 16) & 15u, v = tv ? tv : 5u;
+    if (v == 15u) return (int)g;
+    const uint32_t S = 1u << v, full = gridDim.x / (8u * S) * (8u * S);
+    if (g >= full) return (int)g;
+    const uint32_t i = g >> 3, x = g & 7u;
+    return (int)((((i / S) << 3) + x) * S + i % S);
+}
+
 // The production kernel: rt_fast.h traversal + a flat per-lane segment loop.
 // raytracing_kernel_main / ray_color (main_raytracing.cu:111-200) nest `for sample { for
 // bounce { ... break } }`; on a SIMD machine that makes every lane wait at the end of each
@@ -500,9 +516,10 @@ template <int STACK, bool STATS, int MODE>
 __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* const stk, uint32_t* const scratch) {
     const float4* nodes4 = reinterpret_cast<const float4*>(a.nodes);
     const float4* tris = reinterpret_cast<const float4*>(a.tris);
-    // one 64-lane workgroup per 8x8 sub-tile: tile k = blockIdx / 4, sub-tile blockIdx % 4
-    const int k = (int)blockIdx.x >> 2;
-    const int tid = (((int)blockIdx.x & 3) << 6) | (int)threadIdx.x;
+    // one 64-lane workgroup per 8x8 sub-tile: tile k = lb / 4, sub-tile lb % 4
+    const int lb = xcd_block(a.tune);
+    const int k = lb >> 2;
+    const int tid = ((lb & 3) << 6) | (int)threadIdx.x;
     const int tile = a.shard_index + k * a.shard_count;
     int lx, ly;
     tile_pixel(tid, &lx, &ly);

@@ -1,6 +1,7 @@
 """Per-wave cost distribution of one frame (timing kernel, RT_TUNE=256+2048 must be set in the
 environment): start/end clocks of every 64-pixel wave, for load-balance analysis of the
-multi-GPU split.  Writes gpurun_out/wave_costs.npz and prints a summary."""
+multi-GPU split.  Records are indexed by workgroup (dispatch order); the sub-tile a workgroup
+renders is rt_kernel.hip xcd_block of that index.  Writes gpurun_out/wave_costs.npz and prints a summary."""
 import json
 import os
 import sys
