@@ -4,38 +4,49 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
 
 N = 1 runs BASELINE.json configs[1] (Stanford bunny scene, 1920x1080, 8 spp, 6 bounces).
-N > 1 (launched by torch.distributed.run, one process per GPU): the frame is cut into 16x16
-tiles dealt round-robin over the ranks; each rank renders its tiles into a compact shard, and
-one RCCL gather over xGMI assembles the frame on rank 0, where a kernel un-permutes it into the
-pitched surface.  The gather of frame i runs on its own stream, overlapped with the render of
-frame i+1 (each rank keeps its own shard history, so the next frame does not wait for it).
-  --scaling weak (default): per-GPU work fixed -- the same camera at sqrt(N) x the resolution
-      per axis (N = 4: 3840x2160), so each rank renders about one 1920x1080 frame of tiles.
-  --scaling strong: the 1920x1080 frame itself split N ways.  Its speedup is capped by the
-      heaviest pixel: samples of a pixel share one RNG stream and run in order, and the
-      costliest pixel's 8 samples take ~11 ms alone ("Multi-GPU").
-Timing: barrier + synchronize on both sides of exactly K steps, max over ranks.
+N > 1: one process per GPU.  Launched without a launcher (WORLD_SIZE unset), bench.py starts the
+N rank processes itself before touching the GPU and forwards rank 0's line; under
+torch.distributed.run it is one of the ranks.  The frame's 16x16 tiles are dealt over the ranks
+(--plan cost, the default: a probe frame's per-wave clocks, longest processing time first, each
+rank's heaviest tiles first; --plan rr: round-robin), each rank renders its tiles into a compact
+shard, and ONE gather per frame (rt_gather_shards: RCCL over xGMI, from librt_hip.so) brings the
+shards to rank 0, where rt_unshard_tiles scatters them into the pitched surface.  The gather of
+frame i runs on its own stream, overlapped with the render of frame i+1.
+  --scaling strong (default): the BASELINE frame itself split N ways (the metric's
+      "bunny 1920x1080x8spp @1/2/4/8 GPU"; --config cfg3 is BASELINE configs[2], 4K 64 spp).
+  --scaling weak: per-GPU work fixed -- the same camera at sqrt(N) x the resolution per axis.
+Timing: barrier + synchronize on both sides of exactly K steps, max over ranks; every rank's own
+render-kernel time is reported (rank_kernel_ms).
 
 Rank 0 prints one JSON line.  value = ray segments traced (GetRayHit calls, counted exactly by
-the kernel) per second over the whole job, in Mrays/s.  roofline = the render kernel's
-algorithmic bytes per launch (SURVEY.md section 8(d) formula, from an exact traversal count)
-over its HIP-event-timed average duration, against the 8 TB/s HBM peak.  cpu_baseline = the
-CPU restatement of the reference (oracle/, "port") on this host's cores, same scene and seed.
+the kernel) per second over the whole job, in Mrays/s.
+
+roofline: the render kernel is issue-bound (its ~23 MB scene lives in L2 / Infinity Cache, so HBM
+sees a few GB per frame), so the bound is VALU issue: achieved = SQ_INSTS_VALU per launch (a
+rocprofv3 --pmc pass of this same workload, run by this script as a child process) / the
+kernel's HIP-event time; peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction
+(MI355X_MICROARCH.md: v_fma_f32 wave64 = 2 cycles per SIMD).  Beside it: lane utilisation, the
+effective clock, HBM bytes from FETCH_SIZE x 2 + WRITE_SIZE (the guide's gfx950 correction), and
+the SURVEY.md 8(d) algorithmic-bytes demand figure.
+cpu_baseline = the CPU restatement of the reference (oracle/, "port") on every core this process
+may use on the host (cgroup quota and affinity), same scene and seed; the CPU model is reported.
 """
 import argparse
+import csv
 import glob
 import json
 import os
+import shutil
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-import __graft_entry__ as G  # noqa: E402
 
 CONFIGS = {
     # name: (scene, width, height, spp, bounces, description)
@@ -46,7 +57,18 @@ CONFIGS = {
     "cfg5": ("plane1m", 1920, 1080, 1, 6, "1M-triangle plane 1920x1080 1spp (BASELINE configs[4])"),
 }
 SEED = 0xDEADBEEF
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, memory hierarchy)
+SIMDS = 1024           # 256 CUs x 4 SIMDs
+CLOCK_GHZ = 2.4        # peak engine clock
+VALU_CYCLES = 2        # wave64 fp32 VALU instruction per SIMD (v_fma_f32: 2 cycles, MI355X_MICROARCH.md)
+VALU_PEAK = SIMDS * CLOCK_GHZ / VALU_CYCLES  # G wave-instructions per second
+# PMC passes (rocprofv3 does not split counters over passes; block limits: 8 SQ, 4 TCC, 2 GRBM)
+PMC_PASSES = [
+    ["SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_INSTS_SALU", "SQ_WAVES",
+     "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "GRBM_COUNT"],
+    ["FETCH_SIZE"],
+    ["WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"],
+]
 
 
 def algorithmic_bytes(stats, sphere_count, pixels):
@@ -58,23 +80,27 @@ def algorithmic_bytes(stats, sphere_count, pixels):
     return (32 * nodes + 56 * tris + 32 * sphere_count * seg + 64 * (tacc + sacc) + 36 * tacc + 80 * pixels)
 
 
-def setup_dist(backend="nccl", same_device=False):
-    """One process per GPU (torch.distributed.run sets RANK / LOCAL_RANK / WORLD_SIZE); the
-    "nccl" backend is RCCL on ROCm.  --backend gloo --same-device rehearses the N > 1 path with
-    every rank on GPU 0 (a one-GPU box), staging the gather through host memory."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = 0 if same_device else int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(0)
-    return rank, world
+def usable_cpus():
+    """Cores this process may run on: affinity, capped by the cgroup CPU quota (the GPU box gives
+    a 16-CPU quota on a 256-thread host)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def weak_size(width, height, world):
@@ -92,7 +118,7 @@ def cpu_baseline(cfg, sample_rows=None):
     import rt_testlib as T
 
     scene_name, w, h, spp, bounces, _ = CONFIGS[cfg]
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = usable_cpus()
     osc = T.OracleScene(scene_name)
     rows = sample_rows or h
     if rows >= h:
@@ -106,78 +132,195 @@ def cpu_baseline(cfg, sample_rows=None):
     dt = time.perf_counter() - t
     samples = (r1 - r0) * w * spp
     return {"value": round(float(st[0]) / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "cpu": cpu_model(), "host_threads": os.cpu_count(),
             "sample": f"{cfg} rows [{r0},{r1}) of {h} ({samples} camera samples, {int(st[0])} segments), {dt:.1f} s",
             "samples_per_s": round(samples / dt, 1)}
 
 
-def check_unsharded(rt, scene_name, W, H, spp, bounces, frames, final):
-    """Render the same frames on this GPU without sharding (fresh RNG) and compare bit for bit."""
-    scene = rt.Scene()
-    scene.setup(scene_name)
-    scene.set_viewport(W, H)
-    rng = rt.alloc_rng(W * H)
-    rt.init_rng_states(rng, W, H, SEED)
-    scene.upload(rng.data_ptr())
-    bufs = [rt.alloc_surface(W, H) for _ in range(2)]
-    for i in range(frames):
-        rt.render(scene, bufs[i & 1], bufs[(i + 1) & 1], W, H, spp, bounces, i)
-    torch.cuda.synchronize()
-    # bitwise (same GPU, so NaNs from the reference arithmetic carry the same bits too)
-    a = rt.surface_view(bufs[(frames - 1) & 1], W).contiguous().view(torch.int32)
-    return bool(torch.equal(a, rt.surface_view(final, W).contiguous().view(torch.int32)))
+# ------------------------------------------------------------------------------------------
+# launcher: N rank processes started before any GPU call
+# ------------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
-def load_issue(cfg):
-    """The render kernel's issue-side counters from the committed PMC summary: the path is
-    VALU-issue bound (the scene lives in L2 / Infinity Cache), so the HBM fraction alone does not
-    say how close the kernel is to its limit."""
-    out = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+def launch_ranks(n):
+    """bench.py --gpus N without a launcher: start N rank processes of this script (RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* set), forward rank 0's stdout, return the first failing
+    exit code (and stop the other ranks then)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:  # a dead rank leaves the others waiting in a collective
+                    q.kill()
+        time.sleep(0.05)
+    return rc
+
+
+# ------------------------------------------------------------------------------------------
+# PMC pass (rocprofv3 child process running this script with --pmc-child)
+# ------------------------------------------------------------------------------------------
+def under_profiler():
+    return any(k.startswith("ROCPROF") for k in os.environ)
+
+
+def _short(name):
+    return name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+
+
+def pmc_pass(args, out_dir, timeout_s=150):
+    """Counters of the production render kernel for this workload, one rocprofv3 run per pass;
+    returns {counter: mean per dispatch}, the kernel name and the profiled dispatch time."""
+    rocprof = shutil.which("rocprofv3")
+    if rocprof is None:
+        return None, "rocprofv3 not found"
+    counters, kernel, durations = {}, None, []
+    for i, cs in enumerate(PMC_PASSES):
+        d = os.path.join(out_dir, f"pass{i}")
+        cmd = [rocprof, "--kernel-trace", "--pmc", *cs, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
+               sys.executable, os.path.abspath(__file__), "--pmc-child", "--config", args.config,
+               "--plan", args.plan, "--tune", str(args.tune)]
         try:
-            d = json.load(open(path))
-            c = d["kernels"][d["kernel"]]["counters"]
-        except Exception:
-            continue
-        if d.get("config") == cfg:
-            out = {"bound": "valu", "valu_busy": round(c["VALUBusy"] / 100.0, 3),
-                   "lane_utilization": round(c["VALUUtilization"] / 100.0, 3),
-                   "valu_wave_instructions_per_launch": int(c["SQ_INSTS_VALU"]),
-                   "l2_hit_rate": round(d.get("l2_hit_rate", 0.0), 3),
-                   "source": os.path.relpath(path, ROOT)}
+            r = subprocess.run(cmd, cwd=tempfile.gettempdir(), capture_output=True, text=True, timeout=timeout_s,
+                               env=dict(os.environ, TMPDIR=tempfile.gettempdir()))
+        except subprocess.TimeoutExpired:
+            return None, f"pass {i} timed out"
+        if r.returncode != 0:
+            return None, f"pass {i} exit {r.returncode}: {r.stderr[-300:]}"
+        vals = {}
+        for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for row in csv.DictReader(open(path)):
+                k = _short(row["Kernel_Name"])
+                if not k.startswith("render_fast_kernel"):
+                    continue
+                kernel = k
+                vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+        if i == 0:
+            for path in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+                for row in csv.DictReader(open(path)):
+                    if _short(row["Kernel_Name"]).startswith("render_fast_kernel"):
+                        durations.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
+        if not vals:
+            return None, f"pass {i}: no render_fast_kernel rows"
+        # rows are per dispatch and counter (summed over XCDs by rocprofv3's csv); mean per dispatch
+        for c, v in vals.items():
+            counters[c] = sum(v) / len(v)
+    return {"counters": counters, "kernel": kernel,
+            "profiled_kernel_s": float(np.mean(durations)) if durations else None}, None
+
+
+def roofline(pmc, kern_s, bytes_alg, err=None):
+    out = {"bound": "valu", "unit": "Gwave-instr/s", "peak": round(VALU_PEAK, 1), "achieved": None, "frac": None,
+           "traffic": None, "kernel_ms": round(kern_s * 1e3, 3),
+           "peak_basis": f"{SIMDS} SIMDs x {CLOCK_GHZ} GHz / {VALU_CYCLES} cycles per wave64 VALU instruction",
+           "algorithmic_bytes_per_launch": int(bytes_alg),
+           "algorithmic_demand_gbs": round(bytes_alg / kern_s / 1e9, 1)}
+    if pmc is None:
+        out["pmc_error"] = err
+        return out
+    c = pmc["counters"]
+    valu = c["SQ_INSTS_VALU"]
+    out["kernel"] = pmc["kernel"]
+    out["valu_wave_instructions_per_launch"] = int(valu)
+    out["achieved"] = round(valu / kern_s / 1e9, 1)
+    out["frac"] = round(valu / kern_s / 1e9 / VALU_PEAK, 4)
+    out["lane_utilization"] = round(c["SQ_THREAD_CYCLES_VALU"] / max(1.0, c["SQ_ACTIVE_INST_VALU"] * 64), 4)
+    out["salu_instructions_per_launch"] = int(c["SQ_INSTS_SALU"])
+    tp = pmc.get("profiled_kernel_s")
+    if tp:
+        clk = c["GRBM_GUI_ACTIVE"] / 8 / tp / 1e9  # summed over the 8 XCDs
+        out["clock_ghz"] = round(clk, 3)
+        out["frac_at_clock"] = round(valu * VALU_CYCLES / (SIMDS * clk * 1e9 * tp), 4)
+        out["profiled_kernel_ms"] = round(tp * 1e3, 3)
+    hbm = int((2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024)  # KiB; gfx950 FETCH_SIZE counts half
+    out["traffic"] = hbm
+    out["hbm"] = {"bytes_per_launch": hbm, "achieved_gbs": round(hbm / kern_s / 1e9, 1), "peak_gbs": HBM_PEAK_GBS,
+                  "frac": round(hbm / kern_s / 1e9 / HBM_PEAK_GBS, 4),
+                  "l2_hit_rate": round(c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 4)}
+    out["pmc_counters"] = {k: round(v, 1) for k, v in sorted(c.items())}
     return out
 
 
-def load_traffic(cfg):
-    """HBM bytes per render launch from a committed PMC summary (profiles/*pmc*.json), if any."""
-    best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
-        try:
-            d = json.load(open(path))
-        except Exception:
-            continue
-        if d.get("config") == cfg and "hbm_bytes_per_launch" in d:
-            best = d["hbm_bytes_per_launch"]
-    return best
+# ------------------------------------------------------------------------------------------
+# ranks
+# ------------------------------------------------------------------------------------------
+def setup_dist(backend, same_device):
+    """One process per GPU (RANK / LOCAL_RANK / WORLD_SIZE from the launcher); the "nccl" backend
+    is RCCL on ROCm and only carries set-up and timing collectives (the frame's gather is
+    rt_gather_shards).  --backend gloo --same-device rehearses the N > 1 path with every rank on
+    GPU 0 (a one-GPU box), staging the gather through host memory."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = 0 if same_device else int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return rank, world
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rows", type=int, default=0, help="rows of the frame the CPU baseline renders (0 = auto)")
-    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
-    ap.add_argument("--same-device", action="store_true", help="every rank on GPU 0 (rehearsal on a one-GPU box)")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="N > 1: weak = sqrt(N) x resolution per axis (per-GPU work fixed); strong = same frame")
-    ap.add_argument("--check", action="store_true",
-                    help="after timing, rank 0 re-renders the same frames unsharded and compares the final frame")
-    args = ap.parse_args()
+def make_plan(rt, scene, W, H, SPP, BOUNCES, rank, world, plan_kind, dev):
+    """(tile_lists [world, cap] int32 numpy, counts, probe info).  'cost': every rank renders its
+    round-robin tiles once with per-wave clocks (set-up, untimed, throw-away RNG), the per-tile
+    costs are summed over ranks, and rt_shard_plan deals them longest-first."""
+    import torch
+    import torch.distributed as dist
+
+    if plan_kind == "rr" or world == 1 and plan_kind != "cost":
+        lists, counts = rt.shard_plan(W, H, world)
+        return lists, counts, None
+    rr, rc = rt.shard_plan(W, H, world)
+    mine = torch.from_numpy(rr[rank, : rc[rank]]).to(dev)
+    rng = rt.alloc_rng(int(rc[rank]) * 256)
+    rt.init_rng_tiles(rng, W, H, mine, SEED)
+    shard = torch.zeros((int(rc[rank]) * 256, 4), dtype=torch.float32, device=dev)
+    clocks = torch.zeros(int(rc[rank]) * 4, dtype=torch.int64, device=dev)
+    t0 = time.perf_counter()
+    rt.render(scene, None, None, W, H, SPP, BOUNCES, 0, rank, world, out_shard=shard, tile_list=mine,
+              wave_clock=clocks)
+    torch.cuda.synchronize()
+    probe_s = time.perf_counter() - t0
+    cost = np.zeros(rt.sharding.tiles_total(W, H), dtype=np.float64)
+    cost[rr[rank, : rc[rank]]] = clocks.view(-1, 4).sum(1).double().cpu().numpy()
+    if world > 1:
+        t = torch.from_numpy(cost).to(dev) if dist.get_backend() == "nccl" else torch.from_numpy(cost)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        cost = t.cpu().numpy()
+    lists, counts = rt.shard_plan(W, H, world, cost)
+    del rng, shard, clocks
+    return lists, counts, {"probe_frame_s": round(probe_s, 4), "kind": "cost (probe-frame wave clocks, LPT)"}
+
+
+def run(args):
+    import torch
+    import torch.distributed as dist
+    import __graft_entry__ as G
 
     rank, world = setup_dist(args.backend, args.same_device)
-    assert world == args.gpus or world == 1, f"--gpus {args.gpus} but WORLD_SIZE {world}"
+    assert world == args.gpus or args.pmc_child, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     rt = G.load_package()
     scene_name, W, H, SPP, BOUNCES, desc = CONFIGS[args.config]
     if world > 1 and args.scaling == "weak":
@@ -191,32 +334,54 @@ def main():
     scene.setup(scene_name)
     scene.set_viewport(W, H)
     sharded = world > 1
+    tile_list = None
+    plan_info = None
     if sharded:
-        tiles = rt.shard_tiles(W, H, rank, world)
-        per_shard = max(rt.shard_tiles(W, H, r, world) for r in range(world))
-        rng = rt.alloc_rng(per_shard * 256)
-        rt.init_rng_states(rng, W, H, SEED, rank, world)
-        bufs = [torch.zeros((per_shard * 256, 4), dtype=torch.float32, device=dev) for _ in range(2)]
-        gathered = torch.empty((world, per_shard * 256, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+        # the scene must be uploaded before the probe; RNG pointer is set per buffer below
+        probe_rng = rt.alloc_rng(256)
+        scene.upload(probe_rng.data_ptr())
+        lists, counts, plan_info = make_plan(rt, scene, W, H, SPP, BOUNCES, rank, world, args.plan, dev)
+        cap = lists.shape[1]
+        count = int(counts[rank])
+        tile_list = torch.from_numpy(lists[rank, :count]).to(dev)
+        lists_dev = torch.from_numpy(lists).to(dev)
+        rng = rt.alloc_rng(cap * 256)
+        rt.init_rng_tiles(rng, W, H, tile_list, SEED)
+        bufs = [torch.zeros((cap * 256, 4), dtype=torch.float32, device=dev) for _ in range(2)]
+        gathered = torch.empty((world, cap * 256, 4), dtype=torch.float32, device=dev) if rank == 0 else None
         frame = rt.alloc_surface(W, H) if rank == 0 else None
+        pixels_rank = count * 256
     else:
-        tiles = rt.shard_tiles(W, H, 0, 1)
-        per_shard = tiles
+        if args.plan == "cost":
+            probe_rng = rt.alloc_rng(256)
+            scene.upload(probe_rng.data_ptr())
+            lists, counts, plan_info = make_plan(rt, scene, W, H, SPP, BOUNCES, 0, 1, "cost", dev)
+            tile_list = torch.from_numpy(lists[0, : int(counts[0])]).to(dev)
         rng = rt.alloc_rng(W * H)
         rt.init_rng_states(rng, W, H, SEED)
         bufs = [rt.alloc_surface(W, H) for _ in range(2)]
+        pixels_rank = W * H
     scene.upload(rng.data_ptr())
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
-    pixels_rank = tiles * 256 if sharded else W * H
+
+    def render(i, cur, prev, **kw):
+        if sharded:
+            rt.render(scene, None, prev, W, H, SPP, BOUNCES, i, rank, world, out_shard=cur, tile_list=tile_list,
+                      tune=args.tune, **kw)
+        else:
+            rt.render(scene, cur, prev, W, H, SPP, BOUNCES, i, tile_list=tile_list, tune=args.tune, **kw)
+
+    if args.pmc_child:  # under rocprofv3 --pmc: a warm-up and two frames of the production kernel
+        for i in range(3):
+            render(i, bufs[i & 1], bufs[(i + 1) & 1])
+        torch.cuda.synchronize()
+        return 0
 
     # --- exact traversal counts of one frame (stats kernel variant) on a copy of the RNG state
     rng_saved = rng.clone()
     stats = torch.zeros(24, dtype=torch.int64, device=dev)
-    if sharded:
-        rt.render(scene, None, bufs[1], W, H, SPP, BOUNCES, 0, rank, world, out_shard=bufs[0], stats=stats)
-    else:
-        rt.render(scene, bufs[0], bufs[1], W, H, SPP, BOUNCES, 0, stats=stats)
+    render(0, bufs[0], bufs[1], stats=stats)
     torch.cuda.synchronize()
     rng.copy_(rng_saved)
     del rng_saved
@@ -224,12 +389,23 @@ def main():
     gpu = scene.gpu.contents
     bytes0 = algorithmic_bytes(stats0, gpu.sphere_count, pixels_rank)
 
+    # --- the frame-end gather: rt_gather_shards (RCCL) unless rehearsing on gloo
+    comm = None
+    gather_kind = None
+    if sharded:
+        if args.backend == "nccl" and args.gather == "rccl":
+            obj = [rt.Comm.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            comm = rt.Comm(world, rank, obj[0])
+            gather_kind = "rt_gather_shards (RCCL send/recv group, librt_hip.so)"
+        else:
+            gather_kind = f"torch.distributed.gather ({args.backend})"
+    recv_bytes = [int(c) * 256 * 16 for c in counts] if sharded else None
+
     seg_counter = torch.zeros(1, dtype=torch.int64, device=dev)
     n_total = args.warmup + args.steps
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_total)]
-
-    # gather/render overlap (RCCL only; the gloo rehearsal stages through host memory in line)
-    comm = torch.cuda.Stream() if sharded and args.backend == "nccl" else None
+    comm_stream = torch.cuda.Stream() if comm is not None else None
     rendered = torch.cuda.Event()
     gathered_ev = [torch.cuda.Event(), torch.cuda.Event()]  # the gather that last read bufs[j]
     gather_pending = [False, False]
@@ -239,26 +415,20 @@ def main():
         if comm is not None and gather_pending[i & 1]:
             stream.wait_event(gathered_ev[i & 1])  # frame i-2's gather still reads `cur`
         ev[i][0].record(stream)
-        if sharded:
-            rt.render(scene, None, prev, W, H, SPP, BOUNCES, i, rank, world, out_shard=cur,
-                      segment_counter=seg_counter if i >= args.warmup else None)
-        else:
-            rt.render(scene, cur, prev, W, H, SPP, BOUNCES, i,
-                      segment_counter=seg_counter if i >= args.warmup else None)
+        render(i, cur, prev, segment_counter=seg_counter if i >= args.warmup else None)
         ev[i][1].record(stream)
         if comm is not None:
             rendered.record(stream)
-            comm.wait_event(rendered)
-            with torch.cuda.stream(comm):
-                rt.sharding.gather_shards(cur, rank, world, out=gathered)
-                if rank == 0:
-                    rt.unshard(frame, W, H, world, gathered, per_shard)
-                gathered_ev[i & 1].record(comm)
+            comm_stream.wait_event(rendered)
+            comm.gather(cur, recv_bytes[rank], gathered, cur.numel() * 4, recv_bytes, 0, comm_stream)
+            if rank == 0:
+                rt.unshard_tiles(frame, W, H, gathered, lists_dev, stream=comm_stream)
+            gathered_ev[i & 1].record(comm_stream)
             gather_pending[i & 1] = True
         elif sharded:
-            rt.sharding.gather_shards(cur, rank, world, out=gathered)
+            got = rt.sharding.gather_shards(cur, rank, world, out=gathered)
             if rank == 0:
-                rt.unshard(frame, W, H, world, gathered, per_shard)
+                rt.unshard_tiles(frame, W, H, got, lists_dev)
 
     for i in range(args.warmup):
         step(i)
@@ -278,25 +448,39 @@ def main():
     segs = int(seg_counter.item())
     kern_ms = [ev[i][0].elapsed_time(ev[i][1]) for i in range(args.warmup, n_total)]
     kern_avg_s = float(np.mean(kern_ms)) / 1e3
+    rank_kernel_ms = [kern_avg_s * 1e3]
     if sharded:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        cdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        s = torch.tensor([segs], dtype=torch.int64, device=dev)
+        s = torch.tensor([segs], dtype=torch.int64, device=cdev)
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
         segs_total = int(s.item())
+        km = torch.zeros(world, dtype=torch.float64, device=cdev)
+        km[rank] = kern_avg_s * 1e3
+        dist.all_reduce(km, op=dist.ReduceOp.SUM)
+        rank_kernel_ms = km.cpu().tolist()
     else:
         segs_total = segs
 
-    # algorithmic bytes per timed launch: frame-0 exact counts scaled by the exact segment ratio
     seg_per_launch = segs / args.steps
     bytes_per_launch = bytes0 * (seg_per_launch / max(1, int(stats0[0])))
-    achieved = bytes_per_launch / kern_avg_s / 1e9
-    final = (frame if sharded else bufs[(n_total - 1) & 1])
+    final = frame if sharded else bufs[(n_total - 1) & 1]
+    result = None
     if rank == 0:
         img = rt.surface_view(final, W)
         bad = (~torch.isfinite(img)).any(-1).nonzero()
         finite = bad.shape[0] == 0
+        pmc, err = None, "PMC pass runs at N = 1 only (the rank-0 shard's counters are not the job's)"
+        if world == 1:
+            if args.no_pmc or under_profiler():
+                err = "skipped (--no-pmc or already under a profiler)"
+            else:
+                with tempfile.TemporaryDirectory() as td:
+                    pmc, err = pmc_pass(args, args.pmc_dir or td)
+        roof = roofline(pmc, kern_avg_s, bytes_per_launch, err)
+        roof["frame0_counts"] = {k: int(v) for k, v in zip(rt.STAT_NAMES, stats0) if k and int(v)}
         result = {
             "metric": "Mrays/s + achieved HBM GB/s, Stanford bunny 1920x1080x8spp @1/2/4/8 GPU",
             "value": round(segs_total / elapsed / 1e6, 2),
@@ -306,7 +490,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": args.scaling if sharded else "weak",
+            "scaling": args.scaling if sharded else "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (reference scene: Cornell box + Stanford bunny + HDR sky, seed 0xDEADBEEF)",
@@ -314,15 +498,16 @@ def main():
                        "bounces": BOUNCES, "parallelism": f"tiles{world}" if sharded else "single",
                        "camera_samples_per_s": round(W * H * SPP * args.steps / elapsed, 1),
                        "segments_per_step": round(segs_total / args.steps, 1)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config),
-                         "issue": load_issue(args.config),
-                         "kernel": "render_fast_kernel", "kernel_ms": round(kern_avg_s * 1e3, 3),
-                         "algorithmic_bytes_per_launch": int(bytes_per_launch),
-                         "frame0_counts": {k: int(v) for k, v in zip(rt.STAT_NAMES, stats0) if k}},
+            "roofline": roof,
+            "rank_kernel_ms": [round(x, 3) for x in rank_kernel_ms],
             "setup_s": round(setup_s, 2),
             "image_finite": finite,
         }
+        if plan_info or sharded:
+            result["plan"] = dict(plan_info or {"kind": "round-robin"},
+                                  tiles_per_rank=[int(c) for c in counts] if sharded else None)
+        if gather_kind:
+            result["gather"] = gather_kind
         if not finite:  # (y, x) of non-finite pixels; the reference arithmetic can produce them too
             result["nonfinite_pixels"] = bad[:8].tolist()
         if args.check:
@@ -331,10 +516,63 @@ def main():
             auto_rows = {"cfg1": 256, "cfg2": 1080, "cfg3": 64, "cfg4": 540, "cfg5": 1080}[args.config]
             result["cpu_baseline"] = cpu_baseline(args.config, args.cpu_rows or auto_rows)
         print(json.dumps(result), flush=True)
+    if comm is not None:
+        torch.cuda.synchronize()
+        comm.close()
     if sharded:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
+
+
+def check_unsharded(rt, scene_name, W, H, spp, bounces, frames, final):
+    """Render the same frames on this GPU without sharding (fresh RNG) and compare bit for bit."""
+    import torch
+
+    scene = rt.Scene()
+    scene.setup(scene_name)
+    scene.set_viewport(W, H)
+    rng = rt.alloc_rng(W * H)
+    rt.init_rng_states(rng, W, H, SEED)
+    scene.upload(rng.data_ptr())
+    bufs = [rt.alloc_surface(W, H) for _ in range(2)]
+    for i in range(frames):
+        rt.render(scene, bufs[i & 1], bufs[(i + 1) & 1], W, H, spp, bounces, i)
+    torch.cuda.synchronize()
+    # bitwise (same GPU, so NaNs from the reference arithmetic carry the same bits too)
+    a = rt.surface_view(bufs[(frames - 1) & 1], W).contiguous().view(torch.int32)
+    return bool(torch.equal(a, rt.surface_view(final, W).contiguous().view(torch.int32)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc pass (roofline.frac = null)")
+    ap.add_argument("--pmc-dir", default=None, help="keep the PMC pass's rocprofv3 output here")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-rows", type=int, default=0, help="rows of the frame the CPU baseline renders (0 = auto)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--gather", default="rccl", choices=["rccl", "torch"],
+                    help="frame gather: rt_gather_shards over RCCL (C-ABI) or torch.distributed.gather")
+    ap.add_argument("--same-device", action="store_true", help="every rank on GPU 0 (rehearsal on a one-GPU box)")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="N > 1: strong = the BASELINE frame split N ways; weak = sqrt(N) x resolution per axis")
+    ap.add_argument("--plan", default=None, choices=["cost", "rr"],
+                    help="tile deal: cost (probe-frame clocks, longest first; default for N > 1) or round-robin")
+    ap.add_argument("--tune", type=lambda s: int(s, 0), default=0, help="diagnostic A/B knobs (0 = production)")
+    ap.add_argument("--check", action="store_true",
+                    help="after timing, rank 0 re-renders the same frames unsharded and compares the final frame")
+    args = ap.parse_args()
+    if args.plan is None:
+        args.plan = "cost" if args.gpus > 1 else "rr"
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.pmc_child:
+        return launch_ranks(args.gpus)
+    return run(args)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -64,7 +64,9 @@ class RenderParams(ctypes.Structure):
                 ("width", ctypes.c_int32), ("height", ctypes.c_int32), ("pitch", ctypes.c_uint64),
                 ("frame_index", ctypes.c_int32), ("spp", ctypes.c_int32), ("bounces", ctypes.c_int32),
                 ("shard_index", ctypes.c_int32), ("shard_count", ctypes.c_int32), ("flags", ctypes.c_int32),
-                ("out_shard", ctypes.c_void_p), ("stats", ctypes.c_void_p), ("segment_counter", ctypes.c_void_p)]
+                ("out_shard", ctypes.c_void_p), ("stats", ctypes.c_void_p), ("segment_counter", ctypes.c_void_p),
+                ("tile_list", ctypes.c_void_p), ("tile_count", ctypes.c_int64), ("wave_clock", ctypes.c_void_p),
+                ("tune", ctypes.c_uint32)]
 
 
 assert ctypes.sizeof(GPUScene) == 136 and ctypes.sizeof(GPUMaterial) == 64
@@ -79,10 +81,24 @@ SIGNATURES = {
     "rt_init_rng": (_I, [_P, _I, _I, _I, _I, _U32, _P]),
     "rt_shard_tiles": (ctypes.c_int64, [_I, _I, _I, _I]),
     "rt_unshard": (_I, [_P, _U64, _I, _I, _I, _P, ctypes.c_int64, _P]),
+    "rt_shard_plan_capacity": (ctypes.c_int64, [_I, _I, _I]),
+    "rt_shard_plan": (_I, [_I, _I, _I, _P, ctypes.c_int64, _P, _P]),
+    "rt_init_rng_tiles": (_I, [_P, _I, _I, _P, ctypes.c_int64, _U32, _P]),
+    "rt_unshard_tiles": (_I, [_P, _U64, _I, _I, _I, _P, ctypes.c_int64, _P, _P]),
+    "rt_comm_unique_id": (_I, [_P]),
+    "rt_comm_init_rank": (_I, [ctypes.POINTER(_P), _I, _I, _P]),
+    "rt_comm_init_all": (_I, [_P, _I, _P]),
+    "rt_comm_destroy": (_I, [_P]),
+    "rt_comm_rank": (_I, [_P]),
+    "rt_comm_size": (_I, [_P]),
+    "rt_comm_group_start": (_I, []),
+    "rt_comm_group_end": (_I, []),
+    "rt_gather_shards": (_I, [_P, _P, _SZ, _P, _SZ, _P, _I, _P]),
     "rt_tonemap_srgb8": (_I, [_P, _U64, _I, _I, _P, _P]),
     "rt_write_pfm": (_I, [ctypes.c_char_p, _P, _U64, _I, _I]),
     "rt_write_ppm": (_I, [ctypes.c_char_p, _P, _I, _I]),
     "rt_set_device": (_I, [_I]),
+    "rt_device_count": (_I, []),
     "rt_malloc": (_I, [ctypes.POINTER(_P), _SZ]),
     "rt_malloc_pitch": (_I, [ctypes.POINTER(_P), ctypes.POINTER(_SZ), _SZ, _SZ]),
     "rt_free": (_I, [_P]),
@@ -102,6 +118,7 @@ SIGNATURES = {
     "rt_scene_add_sphere": (None, [_P, _FP, _F, _I]),
     "rt_scene_add_mesh_file": (_I, [_P, ctypes.c_char_p, _FP, _I]),
     "rt_scene_set_environment_file": (_I, [_P, ctypes.c_char_p]),
+    "rt_scene_environment": (_I, [_P, ctypes.POINTER(_P), ctypes.POINTER(_I)]),
     "rt_scene_set_camera": (None, [_P, _FP, _F, _F]),
     "rt_scene_set_viewport": (None, [_P, _I, _I]),
     "rt_scene_upload": (_I, [_P, _P]),
@@ -195,6 +212,16 @@ class Scene:
 
     def set_environment(self, path):
         _check(lib().rt_scene_set_environment_file(self.handle, path.encode()), "set_environment")
+
+    def environment(self):
+        """Host copy of the level-0 cube texels [6, size, size, 4] (None when no sky is set)."""
+        p, n = ctypes.c_void_p(), ctypes.c_int()
+        _check(lib().rt_scene_environment(self.handle, ctypes.byref(p), ctypes.byref(n)), "rt_scene_environment")
+        if not p.value:
+            return None
+        k = n.value
+        buf = ctypes.string_at(p.value, 6 * k * k * 16)
+        return np.frombuffer(buf, dtype=np.float32).reshape(6, k, k, 4).copy()
 
     def setup(self, which="bunny", assets_dir=ASSETS_DIR):
         """CUDARayTracer::SetupCornellBox + SetupStanfordBunny (or the config-4/5 scenes)."""
@@ -299,9 +326,21 @@ def init_rng_states(rng, width, height, seed, shard_index=0, shard_count=1, stre
 
 
 def render(scene, surface, last, width, height, spp, bounces, frame_index=0, shard_index=0, shard_count=1,
-           out_shard=None, stats=None, segment_counter=None, stream=None, tracer="fast"):
-    """rt_render: one frame (or one shard of it) on `stream` (default: torch's current stream)."""
+           out_shard=None, stats=None, segment_counter=None, stream=None, tracer="fast", tile_list=None,
+           wave_clock=None, tune=0):
+    """rt_render: one frame (or one shard of it) on `stream` (default: torch's current stream).
+    tile_list: device int32 tensor of tile ids (a row of a sharding.Plan) instead of the
+    round-robin deal; wave_clock: device int64 tensor [entries*4] receiving per-wave clocks;
+    tune: diagnostic A/B knobs (0 = production)."""
     p = RenderParams()
+    if tile_list is not None:
+        assert tile_list.dtype == torch.int32 and tile_list.is_cuda and tile_list.dim() == 1
+        p.tile_list, p.tile_count = tile_list.data_ptr(), tile_list.numel()
+    if wave_clock is not None:
+        n = tile_list.numel() if tile_list is not None else tiles_of(width, height, shard_index, shard_count)
+        assert wave_clock.dtype == torch.int64 and wave_clock.numel() >= 4 * n
+        p.wave_clock = wave_clock.data_ptr()
+    p.tune = int(tune)
     p.surface = surface.data_ptr() if surface is not None else None
     p.surface_last_frame = last.data_ptr() if last is not None else None
     p.width, p.height = width, height
@@ -330,6 +369,72 @@ def cluster_cull_host(origin, nd, best, node):
 
 def shard_tiles(width, height, shard_index, shard_count):
     return int(lib().rt_shard_tiles(width, height, shard_index, shard_count))
+
+
+tiles_of = shard_tiles
+
+
+def shard_plan(width, height, shard_count, tile_cost=None):
+    """rt_shard_plan: (tile_lists int32 [shard_count, capacity] -1 padded, counts int64 [shard_count])
+    on the host; tile_cost None = round-robin, else longest-processing-time-first."""
+    cap = int(lib().rt_shard_plan_capacity(width, height, shard_count))
+    lists = np.zeros((shard_count, cap), dtype=np.int32)
+    counts = np.zeros((shard_count,), dtype=np.int64)
+    cost_ptr = None
+    if tile_cost is not None:
+        cost = np.ascontiguousarray(tile_cost, dtype=np.float64)
+        assert cost.size == sharding.tiles_total(width, height)
+        cost_ptr = cost.ctypes.data
+    _check(lib().rt_shard_plan(width, height, shard_count, cost_ptr, cap, lists.ctypes.data, counts.ctypes.data),
+           "rt_shard_plan")
+    return lists, counts
+
+
+def init_rng_tiles(rng, width, height, tile_list, seed, stream=None):
+    """rt_init_rng_tiles: compact states for a device int32 tile list."""
+    _check(lib().rt_init_rng_tiles(ctypes.c_void_p(rng.data_ptr()), width, height, ctypes.c_void_p(tile_list.data_ptr()),
+                                   tile_list.numel(), seed, _stream_ptr(stream)), "rt_init_rng_tiles")
+
+
+def unshard_tiles(surface, width, height, shards, tile_lists, stream=None):
+    """rt_unshard_tiles: shards [N, capacity*256, 4] f32, tile_lists device int32 [N, capacity]."""
+    n, cap = tile_lists.shape
+    _check(lib().rt_unshard_tiles(ctypes.c_void_p(surface.data_ptr()), surface.shape[1] * 4, width, height, n,
+                                  ctypes.c_void_p(shards.data_ptr()), cap, ctypes.c_void_p(tile_lists.data_ptr()),
+                                  _stream_ptr(stream)), "rt_unshard_tiles")
+
+
+class Comm:
+    """rt_comm (RCCL) for the frame-end gather.  Rank 0 makes the id (``unique_id()``); the caller
+    hands it to every rank; each rank constructs ``Comm(nranks, rank, id)`` on its device."""
+
+    ID_BYTES = 128
+
+    @staticmethod
+    def unique_id():
+        buf = (ctypes.c_uint8 * Comm.ID_BYTES)()
+        _check(lib().rt_comm_unique_id(buf), "rt_comm_unique_id")
+        return bytes(buf)
+
+    def __init__(self, nranks, rank, uid):
+        assert len(uid) == Comm.ID_BYTES
+        self.handle = ctypes.c_void_p()
+        buf = (ctypes.c_uint8 * Comm.ID_BYTES)(*uid)
+        _check(lib().rt_comm_init_rank(ctypes.byref(self.handle), nranks, rank, buf), "rt_comm_init_rank")
+        self.rank, self.nranks = rank, nranks
+
+    def gather(self, shard, shard_bytes, gathered=None, stride=0, recv_bytes=None, root=0, stream=None):
+        rb = None
+        if recv_bytes is not None:
+            rb = (ctypes.c_size_t * self.nranks)(*[int(b) for b in recv_bytes])
+        _check(lib().rt_gather_shards(self.handle, ctypes.c_void_p(shard.data_ptr()), int(shard_bytes),
+                                      ctypes.c_void_p(gathered.data_ptr() if gathered is not None else None),
+                                      int(stride), rb, root, _stream_ptr(stream)), "rt_gather_shards")
+
+    def close(self):
+        if self.handle:
+            _check(lib().rt_comm_destroy(self.handle), "rt_comm_destroy")
+            self.handle = ctypes.c_void_p()
 
 
 def unshard(surface, width, height, shard_count, shards, per_shard, stream=None):

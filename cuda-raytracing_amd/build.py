@@ -27,8 +27,8 @@ ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 # Numerics flags shared by every translation unit of the product: no FMA contraction, IEEE
 # fp32 division and square root (bit-exact agreement between host code, kernels and oracle).
 FP_FLAGS = ["-ffp-contract=off", "-fno-fast-math"]
-HOST_SOURCES = ["scene.cpp", "objload.cpp", "mirror.cpp", "leaftree.cpp", "xorwow.cpp", "image.cpp"]
-HIP_SOURCES = ["rt_kernel.hip", "image.hip", "bvh_build.hip"]
+HOST_SOURCES = ["scene.cpp", "objload.cpp", "mirror.cpp", "leaftree.cpp", "xorwow.cpp", "image.cpp", "shard.cpp"]
+HIP_SOURCES = ["rt_kernel.hip", "image.hip", "bvh_build.hip", "comm.hip"]
 
 
 def _run(cmd):
@@ -69,7 +69,7 @@ def build_product(force=False):
         list(ex.map(lambda j: _run(j[1]), jobs))
     objs = [o for o, _ in jobs]
     tmp = LIB + ".tmp"
-    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp])
+    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-L/opt/rocm/lib", "-lrccl", "-o", tmp])
     os.replace(tmp, LIB)
     return LIB
 

@@ -40,6 +40,8 @@ struct RenderArgs {
     uint64_t pitch;
     int width, height, frame_index, spp, bounces;
     int shard_index, shard_count, tiles_x;
+    const int32_t* tile_list;        // tile of list entry k (rt_render_params.tile_list) or null: round-robin
+    unsigned long long* wave_clock;  // per-wave elapsed clock ticks, [list entry][4 sub-tiles], or null
     unsigned long long* stats;
     unsigned long long* seg_counter;
     int scene_fast;  // all node bounds inside the filtered-slab range (rt_fast.h)
@@ -48,7 +50,7 @@ struct RenderArgs {
     const float4* ltris;  // their triangle records
     const float4* spairs; // small leaves' triangles in packed pairs, pair (i, i+1) at record i, or null
     const float4* flat;   // leaf trees' flat cluster / cut lists (leaftree.h) or null
-    uint32_t tune;  // A/B knobs (RT_TUNE, rt_render; see rt_fast.h / rt_kernel.hip for the rest: bits 12-15
+    uint32_t tune;  // diagnostic A/B knobs (rt_render_params.tune, 0 in production; see rt_fast.h / rt_kernel.hip for the rest: bits 12-15
                     // split steps, 16-19 XCD run length (rt_kernel.hip xcd_block), 30 per-lane leaf-tree
                     // walk, 31 subtree order):
                     // bit0 no cooperative leaf rounds, bit1 no pair
@@ -64,6 +66,13 @@ struct Counters {
 };
 
 __device__ __forceinline__ rtm::f3 ld3(const float* p) { return rtm::f3{p[0], p[1], p[2]}; }
+
+// Tile rendered by list entry k of a shard: an explicit tile list (cost-ordered plans,
+// rt_shard_plan) or the round-robin deal t = shard_index + k * shard_count.  Entries < 0 are
+// padding (no pixels).
+__device__ __forceinline__ int shard_tile(const RenderArgs& a, int k) {
+    return a.tile_list ? a.tile_list[k] : a.shard_index + k * a.shard_count;
+}
 
 // Tile-local pixel of tile-thread `tid` (0..255): wave w covers the 8x8 sub-tile
 // ((w&1)*8, (w>>1)*8), lane l the pixel (l&7, l>>3) of it.  The compact shard layout and

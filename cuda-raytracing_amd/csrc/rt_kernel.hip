@@ -55,6 +55,10 @@ void rt_internal_set_error(const char* msg) { set_error(msg); }
 // memory shim (utils/CUDAHelper.h:114-156)
 // ---------------------------------------------------------------------------------------
 extern "C" int rt_set_device(int device) { return check(hipSetDevice(device), "hipSetDevice"); }
+extern "C" int rt_device_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
 extern "C" int rt_malloc(void** ptr, size_t bytes) { return check(hipMalloc(ptr, bytes), "hipMalloc"); }
 extern "C" int rt_malloc_pitch(void** ptr, size_t* pitch, size_t width_bytes, size_t height) {
     return check(hipMallocPitch(ptr, pitch, width_bytes, height), "hipMallocPitch");
@@ -396,15 +400,15 @@ __global__ __launch_bounds__(WAVE) void render_kernel(RenderArgs a) {
     const int g = (int)blockIdx.x;
     const int k = g >> 2;
     const int tid = ((g & 3) << 6) | (int)threadIdx.x;  // thread index within the 16x16 tile
-    const int tile = a.shard_index + k * a.shard_count;
+    const int tile = shard_tile(a, k);
     int lx, ly;
     tile_pixel(tid, &lx, &ly);
     const int x = (tile % a.tiles_x) * TILE + lx;
     const int y = (tile / a.tiles_x) * TILE + ly;
     Counters c;
-    if (x < a.width && y < a.height) {  // off-frame lanes stay for the wave reduction
+    if (tile >= 0 && x < a.width && y < a.height) {  // off-frame lanes stay for the wave reduction
         const size_t slot = (size_t)k * (TILE * TILE) + tid;
-        const size_t rng_index = a.shard_count == 1 ? (size_t)y * a.width + x : slot;
+        const size_t rng_index = a.out_shard ? slot : (size_t)y * a.width + x;
         shade_pixel<Tracer, STACK, STATS>(a, stk, x, y, rng_index, slot, c);
     }
     // Segment count (always on: the Mrays/s numerator), one atomic per wave.
@@ -520,15 +524,15 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
     const int lb = xcd_block(a.tune);
     const int k = lb >> 2;
     const int tid = ((lb & 3) << 6) | (int)threadIdx.x;
-    const int tile = a.shard_index + k * a.shard_count;
+    const int tile = shard_tile(a, k);
     int lx, ly;
     tile_pixel(tid, &lx, &ly);
     const int x = (tile % a.tiles_x) * TILE + lx;
     const int y = (tile / a.tiles_x) * TILE + ly;
     Counters c;
-    bool pixel = x < a.width && y < a.height;
+    bool pixel = tile >= 0 && x < a.width && y < a.height;
     const size_t slot = (size_t)k * (TILE * TILE) + tid;
-    rt_rng_state* rs = a.rng + (a.shard_count == 1 ? (size_t)(pixel ? y : 0) * a.width + (pixel ? x : 0) : slot);
+    rt_rng_state* rs = a.rng + (a.out_shard ? slot : (size_t)(pixel ? y : 0) * a.width + (pixel ? x : 0));
     rtm::Xorwow rng{0, 0, 0, 0, 0, 0};
     if (pixel) rng = rtm::Xorwow{rs->d, rs->v[0], rs->v[1], rs->v[2], rs->v[3], rs->v[4]};
     const rtm::f3 cam_o = ld3(a.cam.origin), cam_h = ld3(a.cam.horizontal), cam_v = ld3(a.cam.vertical),
@@ -538,7 +542,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
     bool path = false;
     rtm::f3 ro = cam_o, rd = cam_o, color = rtm::mk(0, 0, 0), thr = rtm::mk(1, 1, 1);
     const bool scene_fast = a.scene_fast != 0;
-    const unsigned long long t_start = (MODE & 8) ? __builtin_amdgcn_s_memtime() : 0;
+    const unsigned long long t_start = ((MODE & 8) || a.wave_clock) ? __builtin_amdgcn_s_memtime() : 0;
 
     for (;;) {
         if (pixel && !path) {
@@ -633,6 +637,8 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
         if ((threadIdx.x & 63) == 0) atomicAdd(a.seg_counter, v);
     }
+    // per-wave cost for cost-aware shard plans (rt_render_params.wave_clock; one store per wave)
+    if (a.wave_clock && threadIdx.x == 0) a.wave_clock[lb] = __builtin_amdgcn_s_memtime() - t_start;
     unsigned long long lane_max = c.l_small;  // the busiest lane's small steps (timing frame)
     if (MODE & 8)
         for (int off = 32; off > 0; off >>= 1) {
@@ -716,7 +722,8 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(6))) void 
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(BLOCK) void init_rng_kernel(rt_rng_state* states, const uint32_t* __restrict__ jump,
                                                          uint32_t seed, int64_t count, int width, int height,
-                                                         int shard_index, int shard_count, int tiles_x) {
+                                                         int shard_index, int shard_count, int tiles_x,
+                                                         const int32_t* __restrict__ tile_list) {
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= count) return;
     uint64_t sub;
@@ -724,11 +731,11 @@ __global__ __launch_bounds__(BLOCK) void init_rng_kernel(rt_rng_state* states, c
         sub = (uint64_t)s;  // reference layout: thread id == state index
     } else {
         const int64_t k = s / BLOCK;
-        const int tile = shard_index + (int)k * shard_count;
+        const int tile = tile_list ? tile_list[k] : shard_index + (int)k * shard_count;
         int lx, ly;
         tile_pixel((int)(s % BLOCK), &lx, &ly);
         const int x = (tile % tiles_x) * TILE + lx, y = (tile / tiles_x) * TILE + ly;
-        if (x >= width || y >= height) return;
+        if (tile < 0 || x >= width || y >= height) return;
         sub = (uint64_t)y * (uint64_t)width + (uint64_t)x;
     }
     uint32_t st[6];
@@ -762,14 +769,14 @@ __global__ __launch_bounds__(BLOCK) void init_rng_kernel(rt_rng_state* states, c
 
 __global__ __launch_bounds__(BLOCK) void unshard_kernel(char* surface, uint64_t pitch, int width, int height,
                                                         int shard_count, const float4* shards, int64_t per_shard,
-                                                        int tiles_x) {
+                                                        int tiles_x, const int32_t* __restrict__ tile_lists) {
     const int rank = blockIdx.y;
     const int64_t k = blockIdx.x;
-    const int tile = rank + (int)k * shard_count;
+    const int tile = tile_lists ? tile_lists[(size_t)rank * per_shard + k] : rank + (int)k * shard_count;
     int lx, ly;
     tile_pixel(threadIdx.x, &lx, &ly);
     const int x = (tile % tiles_x) * TILE + lx, y = (tile / tiles_x) * TILE + ly;
-    if (tile >= tiles_x * ((height + TILE - 1) / TILE) || x >= width || y >= height) return;
+    if (tile < 0 || tile >= tiles_x * ((height + TILE - 1) / TILE) || x >= width || y >= height) return;
     const float4 v = shards[((size_t)rank * per_shard + k) * BLOCK + threadIdx.x];
     *reinterpret_cast<float4*>(surface + (size_t)y * pitch + (size_t)x * 16) = v;
 }
@@ -1009,7 +1016,12 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     a.stats = (unsigned long long*)p->stats;
     a.seg_counter = (unsigned long long*)p->segment_counter;
 
-    const int tiles = tiles_of_shard(p->width, p->height, p->shard_index, p->shard_count);
+    if (p->tile_list && (p->tile_count <= 0 || p->tile_count > (int64_t)1 << 28))
+        return set_error("rt_render: tile_list needs 0 < tile_count < 2^28");
+    if (p->tile_list && !p->out_shard && p->shard_count > 1) return set_error("rt_render: sharded render needs out_shard");
+    a.tile_list = p->tile_list;
+    a.wave_clock = (unsigned long long*)p->wave_clock;
+    const int tiles = p->tile_list ? (int)p->tile_count : tiles_of_shard(p->width, p->height, p->shard_index, p->shard_count);
     if (tiles == 0) return 0;
     const bool want_ref = (p->flags & RT_RENDER_TRACER_REF) != 0;
     MirrorDevice mir;
@@ -1020,20 +1032,16 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     const void* tris = mir.tris;
     const int depth = mir.depth;
     const bool scene_fast = mir.fast;
-    static const char* tune = std::getenv("RT_TUNE");  // A/B knobs (RenderArgs::tune)
-    a.tune = tune ? (uint32_t)std::strtoul(tune, nullptr, 0) : 0u;
+    a.tune = p->tune;  // diagnostic A/B knobs; 0 = the production path
     a.pairs = (a.tune & 2u) ? nullptr : (const float4*)mir.pairs;
     a.tree = (a.tune & 4u) ? nullptr : (const float4*)mir.tree;
     a.ltris = (const float4*)mir.ltris;
     a.spairs = (a.tune & 8u) ? nullptr : (const float4*)mir.spairs;
     a.flat = (const float4*)mir.flat;
-    static const bool force_ref = std::getenv("RT_FORCE_REFERENCE_LAYOUT") != nullptr;  // A/B switch
-    a.tris = force_ref ? nullptr : (const FlatTri*)tris;
+    a.tris = want_ref ? nullptr : (const FlatTri*)tris;
     const bool stats = (p->flags & RT_RENDER_STATS) != 0;
     hipStream_t s = (hipStream_t)stream;
-    static const char* which = std::getenv("RT_TRACER");  // A/B switch: ref | flat | fast (default)
-    const bool want_flat = (p->flags & RT_RENDER_TRACER_FLAT) || (which && std::strcmp(which, "flat") == 0);
-    if (want_ref || (which && std::strcmp(which, "ref") == 0)) a.tris = nullptr;
+    const bool want_flat = (p->flags & RT_RENDER_TRACER_FLAT) != 0;
     a.scene_fast = scene_fast ? 1 : 0;
     hipError_t e;
     if (!a.tris)
@@ -1064,7 +1072,20 @@ extern "C" int rt_init_rng(void* states, int width, int height, int shard_index,
     if (count == 0) return 0;
     const int blocks = (int)((count + BLOCK - 1) / BLOCK);
     hipLaunchKernelGGL(init_rng_kernel, dim3(blocks), dim3(BLOCK), 0, (hipStream_t)stream, (rt_rng_state*)states, jump,
-                       seed, count, width, height, shard_index, sc, tiles_x);
+                       seed, count, width, height, shard_index, sc, tiles_x, (const int32_t*)nullptr);
+    return check(hipGetLastError(), "init_rng_kernel launch");
+}
+
+extern "C" int rt_init_rng_tiles(void* states, int width, int height, const int32_t* tile_list, int64_t tile_count,
+                                 uint32_t seed, void* stream) {
+    if (!states || !tile_list || width <= 0 || height <= 0 || tile_count <= 0 || tile_count > ((int64_t)1 << 28))
+        return set_error("rt_init_rng_tiles: bad arguments");
+    const uint32_t* jump = device_jump_table();
+    if (!jump) return set_error("rt_init_rng_tiles: jump table upload failed");
+    const int64_t count = tile_count * BLOCK;
+    hipLaunchKernelGGL(init_rng_kernel, dim3((unsigned)tile_count), dim3(BLOCK), 0, (hipStream_t)stream,
+                       (rt_rng_state*)states, jump, seed, count, width, height, 0, 1, (width + TILE - 1) / TILE,
+                       tile_list);
     return check(hipGetLastError(), "init_rng_kernel launch");
 }
 
@@ -1073,7 +1094,18 @@ extern "C" int rt_unshard(void* surface, uint64_t pitch, int width, int height, 
     if (!surface || !shards || shard_count <= 0 || per_shard <= 0) return set_error("rt_unshard: bad arguments");
     const int tiles_x = (width + TILE - 1) / TILE;
     hipLaunchKernelGGL(unshard_kernel, dim3((unsigned)per_shard, shard_count), dim3(BLOCK), 0, (hipStream_t)stream,
-                       (char*)surface, pitch, width, height, shard_count, (const float4*)shards, per_shard, tiles_x);
+                       (char*)surface, pitch, width, height, shard_count, (const float4*)shards, per_shard, tiles_x,
+                       (const int32_t*)nullptr);
+    return check(hipGetLastError(), "unshard_kernel launch");
+}
+
+extern "C" int rt_unshard_tiles(void* surface, uint64_t pitch, int width, int height, int shard_count,
+                                const void* shards, int64_t per_shard, const int32_t* tile_lists, void* stream) {
+    if (!surface || !shards || !tile_lists || shard_count <= 0 || per_shard <= 0 || width <= 0 || height <= 0)
+        return set_error("rt_unshard_tiles: bad arguments");
+    hipLaunchKernelGGL(unshard_kernel, dim3((unsigned)per_shard, shard_count), dim3(BLOCK), 0, (hipStream_t)stream,
+                       (char*)surface, pitch, width, height, shard_count, (const float4*)shards, per_shard,
+                       (width + TILE - 1) / TILE, tile_lists);
     return check(hipGetLastError(), "unshard_kernel launch");
 }
 
@@ -1104,7 +1136,7 @@ extern "C" void init_rng(uint32_t thread_block_count, uint32_t thread_block_size
         return;
     }
     hipLaunchKernelGGL(init_rng_kernel, dim3(thread_block_count), dim3(thread_block_size), 0, nullptr,
-                       (rt_rng_state*)states, jump, seed, count, 0, 0, 0, 0, 0);
+                       (rt_rng_state*)states, jump, seed, count, 0, 0, 0, 0, 0, (const int32_t*)nullptr);
     if (check(hipGetLastError(), "init_rng_kernel launch")) std::printf("(init_rng) failed: %s\n", rt_last_error());
 }
 

@@ -653,6 +653,13 @@ int rt_scene_set_environment_file(rt_scene* s, const char* path) {
     s->scene.SetEnvironment(rgba, size);
     return 0;
 }
+int rt_scene_environment(const rt_scene* s, const float** texels, int* size) {
+    if (!s || !texels || !size) return 1;
+    const auto& t = s->scene.EnvironmentTexels();
+    *texels = t.empty() ? nullptr : t.data();
+    *size = s->scene.EnvironmentSize();
+    return 0;
+}
 void rt_scene_set_camera(rt_scene* s, const float p[3], float ax, float ay) {
     s->scene.GetCamera().SetPosition(v3(p));
     s->scene.GetCamera().SetXAndle(ax);

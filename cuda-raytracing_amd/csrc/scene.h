@@ -118,6 +118,8 @@ struct Scene : public GPUScene {
     uint32_t AddMaterial(const Material& material);
     void AddLoadedScene(const LoadedMesh& mesh, const mat4& transform, int default_material = 0);
     void SetEnvironment(const std::vector<float>& rgba_level0, int size);
+    const std::vector<float>& EnvironmentTexels() const { return environment_texels; }
+    int EnvironmentSize() const { return environment_size; }
     void Upload(void* rng_state);
     void BuildHost();
 

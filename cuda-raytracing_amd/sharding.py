@@ -7,8 +7,13 @@ tiles r, r + N, r + 2N, ... into a compact shard [k][256] of float4 (slot = k*25
 gather over RCCL (xGMI) brings the N shards to rank 0, and rt_unshard scatters them back into
 the pitched surface.
 
+Plans: round-robin (above) or cost-aware (rt_shard_plan: longest processing time first from a
+probe frame's per-wave clocks, every rank's heaviest tiles first), passed to the kernels as tile
+lists.  The gather is rt_gather_shards (RCCL, librt_hip.so) on the GPU box; ``gather_shards``
+below is the torch.distributed form used by the gloo rehearsal on CPU.
+
 This module holds the host-side bookkeeping used by bench.py and the gloo tests; the data path
-itself (render into shards, unshard) is the HIP kernels behind the C-ABI.
+itself (render into shards, gather, unshard) is the HIP kernels and RCCL behind the C-ABI.
 """
 import numpy as np
 
@@ -28,13 +33,18 @@ def tiles_of_shard(width, height, shard_index, shard_count):
     return (t - shard_index + shard_count - 1) // shard_count
 
 
-def slot_pixels(width, height, shard_index, shard_count, per_shard=None):
+def slot_pixels(width, height, shard_index, shard_count, per_shard=None, tile_list=None):
     """(x, y) of every slot of a compact shard, -1 for padding slots.
 
-    Slot k*256 + tid holds tile shard_index + k*shard_count; within a tile, wave w = tid >> 6
-    covers the 8x8 sub-tile ((w & 1) * 8, (w >> 1) * 8) and lane l = tid & 63 the pixel
-    (l & 7, l >> 3) of it (rt_common.h tile_pixel)."""
-    k = tiles_of_shard(width, height, shard_index, shard_count)
+    Slot k*256 + tid holds tile shard_index + k*shard_count (or tile_list[k] for an explicit
+    plan, rt_shard_plan; entries < 0 are padding); within a tile, wave w = tid >> 6 covers the
+    8x8 sub-tile ((w & 1) * 8, (w >> 1) * 8) and lane l = tid & 63 the pixel (l & 7, l >> 3) of
+    it (rt_common.h tile_pixel)."""
+    if tile_list is not None:
+        tile_list = np.asarray(tile_list)
+        k = len(tile_list)
+    else:
+        k = tiles_of_shard(width, height, shard_index, shard_count)
     per_shard = k if per_shard is None else per_shard
     tiles_x = (width + TILE - 1) // TILE
     tid = np.arange(TILE_PIXELS)
@@ -44,7 +54,9 @@ def slot_pixels(width, height, shard_index, shard_count, per_shard=None):
     xs = np.full((per_shard, TILE_PIXELS), -1, dtype=np.int64)
     ys = np.full((per_shard, TILE_PIXELS), -1, dtype=np.int64)
     for j in range(k):
-        tile = shard_index + j * shard_count
+        tile = int(tile_list[j]) if tile_list is not None else shard_index + j * shard_count
+        if tile < 0:
+            continue
         x = (tile % tiles_x) * TILE + lx
         y = (tile // tiles_x) * TILE + ly
         ok = (x < width) & (y < height)
@@ -78,14 +90,15 @@ def gather_shards(shard, rank, world, out=None):
     return None
 
 
-def unshard_host(shards, width, height):
-    """numpy restatement of rt_unshard (test use): [world, per_shard*256, 4] -> [H, W, 4]."""
+def unshard_host(shards, width, height, tile_lists=None):
+    """numpy restatement of rt_unshard / rt_unshard_tiles (test use): [world, per_shard*256, 4]
+    -> [H, W, 4]."""
     world, n, c = shards.shape
     per_shard = n // TILE_PIXELS
     img = np.zeros((height, width, c), dtype=shards.dtype)
     seen = np.zeros((height, width), dtype=np.int64)
     for r in range(world):
-        xs, ys = slot_pixels(width, height, r, world, per_shard)
+        xs, ys = slot_pixels(width, height, r, world, per_shard, None if tile_lists is None else tile_lists[r])
         ok = xs >= 0
         img[ys[ok], xs[ok]] = shards[r][ok]
         np.add.at(seen, (ys[ok], xs[ok]), 1)

@@ -166,7 +166,21 @@ typedef struct rt_render_params {
     void* out_shard;               /* if non-NULL: compact [k][16*16] float4 shard output */
     uint64_t* stats;               /* RT_RENDER_STATS: RT_STAT_COUNT uint64 counters (zeroed by caller) */
     uint64_t* segment_counter;     /* optional: += ray segments traced (GetRayHit calls) */
+    /* Explicit tile list (cost-aware plans, rt_shard_plan): list entry k renders the row-major
+     * 16x16 tile tile_list[k] (DEVICE int32 array, tile_count entries, < 0 = padding) instead of
+     * the round-robin tile shard_index + k * shard_count.  NULL = round-robin. */
+    const int32_t* tile_list;
+    int64_t tile_count;
+    /* Optional DEVICE uint64 [entries][4]: elapsed shader-clock ticks of each 8x8 sub-tile wave
+     * of the production tracer (the cost input of rt_shard_plan). */
+    uint64_t* wave_clock;
+    uint32_t tune;                 /* diagnostic A/B knobs (tools/); 0 = the production path */
 } rt_render_params;
+
+/* Layout rule: with out_shard set, RNG state s and output s are compact in list order
+ * (state/slot k*256 + t for thread t of list entry k); without it, RNG states are indexed
+ * y*width + x (the reference's layout) and the output goes to the pitched surface, whatever the
+ * tile order. */
 
 #define RT_RENDER_STATS 1          /* count traversal work (slower kernel variant) */
 #define RT_RENDER_TRACER_REF 2     /* force the reference-layout tracer (A/B, tests) */
@@ -221,6 +235,47 @@ int rt_unshard(void* surface, uint64_t pitch, int width, int height, int shard_c
                int64_t tiles_per_shard_max, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Multi-GPU split (the reference renders one frame on one device,
+ * RayTracing/RayTracing.cpp:205-234).  Plans deal 16x16 tiles to ranks; each rank renders a
+ * compact shard; one gather per frame; the root un-permutes.
+ * ------------------------------------------------------------------------------------- */
+/* Entries per rank a plan may use (the row length of tile_lists below). */
+int64_t rt_shard_plan_capacity(int width, int height, int shard_count);
+/* Fill HOST tile_lists [shard_count][capacity] (-1 padded) and counts [shard_count].
+ * tile_cost (HOST, one per row-major tile) NULL = round-robin (rank r: tiles r, r+N, ...);
+ * otherwise longest-processing-time-first: heaviest tile first, each to the least-loaded rank
+ * below capacity; every rank's list comes out heaviest first.  Deterministic.  0 or error. */
+int rt_shard_plan(int width, int height, int shard_count, const double* tile_cost, int64_t capacity,
+                  int32_t* tile_lists, int64_t* counts);
+/* rt_init_rng for an explicit tile list (DEVICE int32): state k*256 + t <- curand_init(seed,
+ * pixel id of thread t of tile tile_list[k]). */
+int rt_init_rng_tiles(void* rng_states, int width, int height, const int32_t* tile_list, int64_t tile_count,
+                      uint32_t seed, void* stream);
+/* rt_unshard with explicit plans: tile_lists is the DEVICE copy of rt_shard_plan's output. */
+int rt_unshard_tiles(void* surface, uint64_t pitch, int width, int height, int shard_count, const void* shards,
+                     int64_t tiles_per_shard_max, const int32_t* tile_lists, void* stream);
+
+/* RCCL communicator for the frame-end gather (csrc/comm.hip).  One process per GPU: rank 0 makes
+ * an id, the host passes it to every rank by its own means, each rank calls rt_comm_init_rank on
+ * its current device.  One process driving N devices: rt_comm_init_all. */
+#define RT_COMM_ID_BYTES 128
+typedef struct rt_comm rt_comm;
+int rt_comm_unique_id(uint8_t id[RT_COMM_ID_BYTES]);
+int rt_comm_init_rank(rt_comm** comm, int nranks, int rank, const uint8_t id[RT_COMM_ID_BYTES]);
+int rt_comm_init_all(rt_comm** comms, int ndev, const int* devices);
+int rt_comm_destroy(rt_comm* comm);
+int rt_comm_rank(const rt_comm* comm);
+int rt_comm_size(const rt_comm* comm);
+/* Bracket the per-device gathers of a one-process, N-device host (RCCL group semantics). */
+int rt_comm_group_start(void);
+int rt_comm_group_end(void);
+/* The frame's gather on `stream`: every rank passes its shard (shard_bytes); the root receives
+ * rank r's bytes at gathered + r * stride (recv_bytes[r] bytes, or shard_bytes for every rank
+ * when recv_bytes is NULL; the root's own shard is copied on the stream).  Asynchronous. */
+int rt_gather_shards(rt_comm* comm, const void* shard, size_t shard_bytes, void* gathered, size_t stride,
+                     const size_t* recv_bytes, int root, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Frame output (the viewer path: main.cpp:66-94 draws the surface with exposure 0.5 + ACES film
  * into an sRGB back buffer, main.cpp:438).  For looking at frames; not on the render path.
  * ------------------------------------------------------------------------------------- */
@@ -236,6 +291,8 @@ int rt_write_ppm(const char* path, const uint8_t* rgb, int width, int height);
  * Device memory / texture shim (replaces utils/CUDAHelper.h and utils/CUDATexture.*).
  * ------------------------------------------------------------------------------------- */
 int rt_set_device(int device);
+/* Visible HIP devices (0 when none or on error). */
+int rt_device_count(void);
 int rt_malloc(void** ptr, size_t bytes);
 int rt_malloc_pitch(void** ptr, size_t* pitch, size_t width_bytes, size_t height);
 int rt_free(void* ptr);
@@ -266,10 +323,18 @@ void rt_scene_add_quad(rt_scene* scene, const float a[3], const float b[3], cons
 void rt_scene_add_sphere(rt_scene* scene, const float position[3], float radius, int material);
 /* Scene::AddLoadedScene with a mesh file -- a Wavefront .obj (imported like the reference's
  * assimp post-processing, objload.cpp) or a mesh asset (assets/bunny_mesh.bin format) -- and a
- * column-major 4x4 transform.  Returns 0 or an error code. */
+ * column-major 4x4 transform.  Returns 0 or an error code.
+ * PARITY NOTE: a scene built from an .obj is NOT a parity scene.  Positions, vertex order and
+ * faces are bit-identical to an assimp 3.3 import, but the smoothed normals differ from it in
+ * the last ulps (assimp's summation order over coincident corners follows its SpatialSort's
+ * unstable sort, and the reference pins no assimp version: vcpkg.json:4-7), so frames rendered
+ * from it can diverge from the reference's.  The parity scenes (rt_scene_setup, the tests and
+ * the benchmark) load the mesh asset, which holds the assimp 3.3 import verbatim. */
 int rt_scene_add_mesh_file(rt_scene* scene, const char* path, const float transform[16], int material);
 /* Environment cube map from an asset (assets/sunset_cube128.bin) or a legacy fp32 DDS. */
 int rt_scene_set_environment_file(rt_scene* scene, const char* path);
+/* Host view of the scene's level-0 cube texels [6][size][size][4] (NULL / 0 when none). */
+int rt_scene_environment(const rt_scene* scene, const float** texels, int* size);
 void rt_scene_set_camera(rt_scene* scene, const float position[3], float angle_x_deg, float angle_y_deg);
 void rt_scene_set_viewport(rt_scene* scene, int width, int height);
 /* Scene::Upload: builds the BVH when dirty, uploads dirty buffers, fills the GPUScene. */

@@ -4,10 +4,17 @@
 // raytracing_process(surface, last, ...) followed by the D2D copy of surface into last.
 // Writes the final frame (W*H float4, rows bottom-up, pitch removed) to argv[1].
 //
+// With a sixth argument "split", the same frames are split over every visible device by the
+// C-ABI's multi-GPU path (one host thread, N devices): rt_shard_plan deals the 16x16 tiles,
+// each device renders its compact shard (spp 5, 6 bounces as raytracing_process), and
+// rt_gather_shards (RCCL, communicators from rt_comm_init_all) brings the shards to device 0,
+// where rt_unshard_tiles writes the pitched surface.
+//
 //   g++ -std=c++17 -Iinclude tests/cpp/host_driver.cpp -Lcuda-raytracing_amd -lrt_hip -o host_driver
-//   ./host_driver out.bin W H frames assets_dir
+//   ./host_driver out.bin W H frames assets_dir [split]
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "rt_abi.h"
@@ -20,14 +27,18 @@
         }                                                                     \
     } while (0)
 
-int main(int argc, char** argv) {
-    if (argc < 6) {
-        std::fprintf(stderr, "usage: %s out.bin W H frames assets_dir\n", argv[0]);
-        return 2;
-    }
-    const int w = std::atoi(argv[2]), h = std::atoi(argv[3]), frames = std::atoi(argv[4]);
+static void write_frame(const char* path, const void* surface, size_t pitch, int w, int h) {
+    std::vector<char> img(pitch * h);
+    CHECK(rt_memcpy_d2h(img.data(), surface, img.size()));
+    FILE* out = std::fopen(path, "wb");
+    if (!out) std::exit(1);
+    for (int y = 0; y < h; y++) std::fwrite(img.data() + (size_t)y * pitch, 16, (size_t)w, out);
+    std::fclose(out);
+}
+
+static int run_single(const char* path, int w, int h, int frames, const char* assets) {
     rt_scene* scene = rt_scene_create();
-    CHECK(rt_scene_setup(scene, 0, argv[5]));  // Cornell box + bunny, RayTracing.cpp:24-25
+    CHECK(rt_scene_setup(scene, 0, assets));  // Cornell box + bunny, RayTracing.cpp:24-25
     rt_scene_set_viewport(scene, w, h);
     // RayTracing.cpp:216-221: the RNG states, seeded per pixel
     const uint32_t block = 128, blocks = (uint32_t)((w * h + block - 1) / block);
@@ -46,16 +57,118 @@ int main(int argc, char** argv) {
         CHECK(rt_memcpy_d2d(last, surface, pitch * h));  // RayTracing.cpp:233
     }
     CHECK(rt_synchronize());
-    std::vector<char> img(pitch * h);
-    CHECK(rt_memcpy_d2h(img.data(), surface, img.size()));
-    FILE* out = std::fopen(argv[1], "wb");
-    if (!out) return 1;
-    for (int y = 0; y < h; y++) std::fwrite(img.data() + (size_t)y * pitch, 16, (size_t)w, out);
-    std::fclose(out);
+    write_frame(path, surface, pitch, w, h);
     rt_free(surface);
     rt_free(last);
     rt_free(rng);
     rt_scene_destroy(scene);
     std::printf("ok %dx%d frames=%d pitch=%zu\n", w, h, frames, pitch);
     return 0;
+}
+
+struct Rank {
+    rt_scene* scene = nullptr;
+    void *rng = nullptr, *shard[2] = {nullptr, nullptr}, *tiles = nullptr;
+    int64_t count = 0;
+};
+
+static int run_split(const char* path, int w, int h, int frames, const char* assets) {
+    const int n = rt_device_count();
+    if (n <= 0) {
+        std::fprintf(stderr, "no HIP device\n");
+        return 1;
+    }
+    std::vector<int> devs(n);
+    for (int d = 0; d < n; d++) devs[d] = d;
+    std::vector<rt_comm*> comms(n, nullptr);
+    CHECK(rt_comm_init_all(comms.data(), n, devs.data()));
+    const int64_t cap = rt_shard_plan_capacity(w, h, n);
+    std::vector<int32_t> lists((size_t)cap * n);
+    std::vector<int64_t> counts(n);
+    CHECK(rt_shard_plan(w, h, n, nullptr, cap, lists.data(), counts.data()));
+    const size_t shard_bytes = (size_t)cap * 256 * 16;
+    std::vector<Rank> ranks(n);
+    std::vector<size_t> recv_bytes(n);
+    for (int d = 0; d < n; d++) {
+        Rank& r = ranks[d];
+        CHECK(rt_set_device(d));
+        r.count = counts[d];
+        recv_bytes[d] = (size_t)r.count * 256 * 16;
+        r.scene = rt_scene_create();
+        CHECK(rt_scene_setup(r.scene, 0, assets));
+        rt_scene_set_viewport(r.scene, w, h);
+        CHECK(rt_malloc(&r.tiles, (size_t)cap * 4));
+        CHECK(rt_memcpy_h2d(r.tiles, lists.data() + (size_t)d * cap, (size_t)cap * 4));
+        CHECK(rt_malloc(&r.rng, (size_t)cap * 256 * 48));
+        CHECK(rt_init_rng_tiles(r.rng, w, h, (const int32_t*)r.tiles, r.count, 0xDEADBEEFu, nullptr));
+        CHECK(rt_scene_upload(r.scene, r.rng));
+        for (int b = 0; b < 2; b++) {
+            CHECK(rt_malloc(&r.shard[b], shard_bytes));
+            CHECK(rt_memset(r.shard[b], 0, shard_bytes));
+        }
+    }
+    CHECK(rt_set_device(0));
+    void *gathered = nullptr, *surface = nullptr, *lists_dev = nullptr;
+    size_t pitch = 0;
+    CHECK(rt_malloc(&gathered, shard_bytes * n));
+    CHECK(rt_malloc(&lists_dev, lists.size() * 4));
+    CHECK(rt_memcpy_h2d(lists_dev, lists.data(), lists.size() * 4));
+    CHECK(rt_malloc_pitch(&surface, &pitch, (size_t)w * 16, h));
+    for (int f = 0; f < frames; f++) {
+        for (int d = 0; d < n; d++) {
+            Rank& r = ranks[d];
+            CHECK(rt_set_device(d));
+            rt_render_params p;
+            std::memset(&p, 0, sizeof(p));
+            p.surface_last_frame = r.shard[(f + 1) & 1];
+            p.width = w, p.height = h, p.frame_index = f;
+            p.spp = 5, p.bounces = 6;  // raytracing_process's constants (main_raytracing.cu:115,166-170)
+            p.shard_index = d, p.shard_count = n;
+            p.out_shard = r.shard[f & 1];
+            p.tile_list = (const int32_t*)r.tiles;
+            p.tile_count = r.count;
+            CHECK(rt_render(&p, rt_scene_gpu(r.scene), nullptr));
+        }
+        CHECK(rt_comm_group_start());
+        for (int d = 0; d < n; d++) {
+            CHECK(rt_set_device(d));
+            CHECK(rt_gather_shards(comms[d], ranks[d].shard[f & 1], recv_bytes[d], d == 0 ? gathered : nullptr,
+                                   shard_bytes, d == 0 ? recv_bytes.data() : nullptr, 0, nullptr));
+        }
+        CHECK(rt_comm_group_end());
+        CHECK(rt_set_device(0));
+        CHECK(rt_unshard_tiles(surface, pitch, w, h, n, gathered, cap, (const int32_t*)lists_dev, nullptr));
+    }
+    for (int d = 0; d < n; d++) {
+        CHECK(rt_set_device(d));
+        CHECK(rt_synchronize());
+    }
+    CHECK(rt_set_device(0));
+    write_frame(path, surface, pitch, w, h);
+    for (int d = 0; d < n; d++) {
+        Rank& r = ranks[d];
+        CHECK(rt_set_device(d));
+        rt_free(r.rng);
+        rt_free(r.tiles);
+        rt_free(r.shard[0]);
+        rt_free(r.shard[1]);
+        rt_scene_destroy(r.scene);
+        CHECK(rt_comm_destroy(comms[d]));
+    }
+    CHECK(rt_set_device(0));
+    rt_free(gathered);
+    rt_free(lists_dev);
+    rt_free(surface);
+    std::printf("ok split %dx%d frames=%d devices=%d\n", w, h, frames, n);
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 6) {
+        std::fprintf(stderr, "usage: %s out.bin W H frames assets_dir [split]\n", argv[0]);
+        return 2;
+    }
+    const int w = std::atoi(argv[2]), h = std::atoi(argv[3]), frames = std::atoi(argv[4]);
+    if (argc > 6 && std::strcmp(argv[6], "split") == 0) return run_split(argv[1], w, h, frames, argv[5]);
+    return run_single(argv[1], w, h, frames, argv[5]);
 }

@@ -20,10 +20,13 @@ def test_host_driver_built():
 
 
 @pytest.mark.gpu
-def test_cpp_host_progressive_frames(tmp_path):
+@pytest.mark.parametrize("mode", ["single", "split"])
+def test_cpp_host_progressive_frames(tmp_path, mode):
+    """single: the reference's call pattern; split: the same frames over every visible device
+    (rt_shard_plan + rt_render shards + rt_gather_shards over RCCL + rt_unshard_tiles)."""
     w, h, frames = 48, 32, 2
     out = tmp_path / "frame.bin"
-    r = subprocess.run([DRIVER, str(out), str(w), str(h), str(frames), os.path.join(T.ROOT, "assets")],
+    r = subprocess.run([DRIVER, str(out), str(w), str(h), str(frames), os.path.join(T.ROOT, "assets"), mode],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     got = np.fromfile(out, dtype=np.float32).reshape(h, w, 4)

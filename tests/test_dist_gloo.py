@@ -29,37 +29,58 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, frame, result_q):
+def _tile_cost(frame):
+    """A deterministic stand-in for the probe frame's per-tile clocks: the tile's summed RGB."""
+    th, tw = (H + 15) // 16, (W + 15) // 16
+    pad = np.zeros((th * 16, tw * 16), dtype=np.float64)
+    pad[:H, :W] = np.nan_to_num(frame[..., :3].sum(-1), nan=1.0, posinf=1.0)
+    return pad.reshape(th, 16, tw, 16).sum((1, 3)).reshape(-1) + 1.0
+
+
+def _worker(rank, world, port, frame, result_q, plan):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         rt = T.load_rt()
         sh = rt.sharding
-        per_shard = max(sh.tiles_of_shard(W, H, r, world) for r in range(world))
-        assert rt.shard_tiles(W, H, rank, world) == sh.tiles_of_shard(W, H, rank, world)
-        xs, ys = sh.slot_pixels(W, H, rank, world, per_shard)
+        if plan == "rr":
+            per_shard = max(sh.tiles_of_shard(W, H, r, world) for r in range(world))
+            assert rt.shard_tiles(W, H, rank, world) == sh.tiles_of_shard(W, H, rank, world)
+            lists = None
+            xs, ys = sh.slot_pixels(W, H, rank, world, per_shard)
+        else:
+            # bench.py's cost plan: each rank measures its round-robin tiles, the costs are summed
+            # over ranks (the set-up collective), and every rank computes the same LPT plan
+            rr, rc = rt.shard_plan(W, H, world)
+            cost = np.zeros(sh.tiles_total(W, H))
+            cost[rr[rank, : rc[rank]]] = _tile_cost(frame)[rr[rank, : rc[rank]]]
+            t = torch.from_numpy(cost)
+            dist.all_reduce(t)
+            lists, counts = rt.shard_plan(W, H, world, t.numpy())
+            per_shard = lists.shape[1]
+            xs, ys = sh.slot_pixels(W, H, rank, world, per_shard, lists[rank, : counts[rank]])
         shard = np.zeros((per_shard * sh.TILE_PIXELS, 4), dtype=np.float32)
         ok = xs >= 0
         shard[ok] = frame[ys[ok], xs[ok]]
         got = sh.gather_shards(torch.from_numpy(shard), rank, world)
         if rank == 0:
-            img, seen = sh.unshard_host(got.numpy(), W, H)
+            img, seen = sh.unshard_host(got.numpy(), W, H, lists)
             result_q.put((img, seen))
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gather_reassembles_frame(world):
+@pytest.mark.parametrize("world,plan", [(2, "rr"), (3, "rr"), (2, "cost"), (3, "cost")])
+def test_gather_reassembles_frame(world, plan):
     osc = T.OracleScene("bunny")
     frame = osc.render(W, H, 1, 2, rng=T.oracle_rng_frame(0xDEADBEEF, W, H, 4), threads=4)
     frame = np.ascontiguousarray(frame.reshape(H, W, 4), dtype=np.float32)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, frame, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, frame, q, plan)) for r in range(world)]
     for p in procs:
         p.start()
     img, seen = q.get(timeout=240)
@@ -98,3 +119,48 @@ def test_weak_scaling_frame_sizes():
         w, h = bench.weak_size(1920, 1080, n)
         assert w % 16 == 0 and abs(w / h - 16 / 9) < 2e-3
         assert abs(w * h / (1920 * 1080 * n) - 1.0) < 0.01
+
+
+def test_shard_plan_round_robin_is_the_deal():
+    rt = T.load_rt()
+    for (w, h, n) in [(1920, 1080, 8), (72, 40, 3), (17, 1, 2), (256, 256, 1)]:
+        lists, counts = rt.shard_plan(w, h, n)
+        assert lists.shape[1] == rt.lib().rt_shard_plan_capacity(w, h, n)
+        for r in range(n):
+            assert counts[r] == rt.shard_tiles(w, h, r, n)
+            assert list(lists[r, : counts[r]]) == list(range(r, rt.sharding.tiles_total(w, h), n))
+            assert (lists[r, counts[r]:] == -1).all()
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+def test_shard_plan_lpt(n):
+    """Longest processing time first: every tile exactly once, within capacity, each rank's list
+    heaviest first, loads within one tile's cost of each other, deterministic."""
+    rt = T.load_rt()
+    w, h = 1920, 1080
+    tiles = rt.sharding.tiles_total(w, h)
+    rng = np.random.default_rng(n)
+    cost = rng.gamma(0.5, 1.0, tiles) * np.where(rng.random(tiles) < 0.05, 20.0, 1.0)
+    lists, counts = rt.shard_plan(w, h, n, cost)
+    cap = lists.shape[1]
+    assert (counts <= cap).all() and counts.sum() == tiles
+    got = np.concatenate([lists[r, : counts[r]] for r in range(n)])
+    assert np.array_equal(np.sort(got), np.arange(tiles))
+    loads = np.array([cost[lists[r, : counts[r]]].sum() for r in range(n)])
+    assert loads.max() - loads.min() <= cost.max() + 1e-9
+    for r in range(n):
+        c = cost[lists[r, : counts[r]]]
+        assert (np.diff(c) <= 0).all()
+    again, _ = rt.shard_plan(w, h, n, cost)
+    assert np.array_equal(again, lists)
+
+
+def test_shard_plan_rejects_bad_costs():
+    rt = T.load_rt()
+    cost = np.ones(rt.sharding.tiles_total(64, 64))
+    cost[3] = np.nan
+    with pytest.raises(rt.RTError):
+        rt.shard_plan(64, 64, 2, cost)
+    cost[3] = -1.0
+    with pytest.raises(rt.RTError):
+        rt.shard_plan(64, 64, 2, cost)

@@ -1,0 +1,129 @@
+"""Full-size parity on every BASELINE configuration: the production kernel through the C-ABI
+against the CPU oracle (oracle/rt_oracle.c, the reference's arithmetic at IEEE fp32), whole
+frames where the oracle finishes in seconds on the GPU box's host cores, deterministic row bands
+spread over the frame where it does not.
+
+    config 1  256x256, 1 spp, 1 bounce        every pixel
+    config 2  1920x1080, 8 spp, 6 bounces     every pixel
+    config 3  3840x2160, 64 spp               8 bands of 17 rows (1/16 of the frame)
+    config 4  4-bunny, 1920x1080, 8 spp       8 bands of 17 rows (1/8) against the oracle, and the
+                                              whole frame against the GPU reference-layout tracer
+                                              (the straight restatement, oracle-checked above)
+    config 5  1M-triangle plane, 1 spp        every pixel
+
+Tolerance: north_star allows |delta RGB| <= 1e-4 per channel; both sides run the same IEEE fp32
+operations in the same order, so the tests assert bit equality (max |delta| = 0, no differing
+value) and print both figures.  Reference: RayTracing/main_raytracing.cu:162-200 (the frame),
+:111-160 (ray_color), :33-109 (GetRayHit / BVHRayHit).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import rt_testlib as T
+
+pytestmark = pytest.mark.gpu
+SUMMARY = os.path.join(T.ROOT, "gpurun_out", "parity_summary.jsonl")
+
+
+@pytest.fixture(scope="module")
+def rt():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    torch.cuda.set_device(0)
+    return T.load_rt()
+
+
+def threads():
+    import bench
+    return bench.usable_cpus()
+
+
+def render_gpu(rt, which, w, h, spp, bounces, tracer="fast"):
+    s = rt.Scene()
+    s.setup(which)
+    s.set_viewport(w, h)
+    rng = rt.alloc_rng(w * h)
+    rt.init_rng_states(rng, w, h, T.SEED)
+    s.upload(rng.data_ptr())
+    a, b = rt.alloc_surface(w, h), rt.alloc_surface(w, h)
+    rt.render(s, a, b, w, h, spp, bounces, tracer=tracer)
+    torch.cuda.synchronize()
+    return rt.surface_view(a, w).cpu().numpy().copy(), rng.view(-1, 12)[:, :6].cpu().numpy().view(np.uint32).copy()
+
+
+def bands(h, count, rows):
+    """`count` bands of `rows` rows spread evenly over the frame (deterministic)."""
+    out = []
+    for i in range(count):
+        r0 = min(h - rows, (i * h) // count + (h // count - rows) // 2)
+        out.append((r0, r0 + rows))
+    return out
+
+
+def report(name, got, want, extra=None):
+    """Bit comparison (NaN positions must agree; other values bit-equal) + printed summary."""
+    nan_g, nan_w = np.isnan(got), np.isnan(want)
+    same_nan = bool(np.array_equal(nan_g, nan_w))
+    if same_nan:
+        g, w = got[~nan_g], want[~nan_w]
+        diff = np.abs(g.astype(np.float64) - w.astype(np.float64))
+        mism = int((g.view(np.uint32) != w.view(np.uint32)).sum())
+    else:
+        diff, mism = np.array([np.inf]), -1
+    rec = {"test": name, "values": int(got.size), "max_abs_delta": float(diff.max()) if diff.size else 0.0,
+           "differing_values": mism, "nan_values": int(nan_w.sum()), "nan_positions_equal": same_nan}
+    rec.update(extra or {})
+    print("PARITY " + json.dumps(rec))
+    if os.path.isdir(os.path.dirname(SUMMARY)):
+        with open(SUMMARY, "a") as f:
+            f.write(json.dumps(rec) + "\n")
+    assert same_nan, f"{name}: NaN positions differ"
+    assert rec["max_abs_delta"] <= 1e-4, f"{name}: max |delta| = {rec['max_abs_delta']}"
+    assert mism == 0, f"{name}: {mism} values differ (max |delta| {rec['max_abs_delta']:.3g}); expected bit-exact"
+
+
+@pytest.mark.parametrize("cfg,which,w,h,spp,bounces", [
+    ("config1", "bunny", 256, 256, 1, 1),
+    ("config2", "bunny", 1920, 1080, 8, 6),
+    ("config5", "plane1m", 1920, 1080, 1, 6),
+])
+def test_full_frame_vs_oracle(rt, cfg, which, w, h, spp, bounces):
+    got, grng = render_gpu(rt, which, w, h, spp, bounces)
+    o = T.OracleScene(which)
+    orng = T.oracle_rng_frame(T.SEED, w, h, threads())
+    want = o.render(w, h, spp, bounces, rng=orng, threads=threads())
+    report(f"{cfg} full frame {w}x{h} {spp}spp", got, want)
+    # the per-pixel RNG states after the frame (the draw count of every pixel's paths)
+    assert np.array_equal(grng, orng.reshape(-1, 6)), f"{cfg}: final RNG states differ"
+
+
+@pytest.mark.parametrize("cfg,which,w,h,spp,count", [
+    ("config3", "bunny", 3840, 2160, 64, 8),    # 8 x 17 rows = 1/16 of the frame
+    ("config4", "bunny4", 1920, 1080, 8, 8),    # 8 x 17 rows = 1/8 of the frame
+])
+def test_row_bands_vs_oracle(rt, cfg, which, w, h, spp, count):
+    got, _ = render_gpu(rt, which, w, h, spp, 6)
+    o = T.OracleScene(which)
+    orng = T.oracle_rng_frame(T.SEED, w, h, threads())
+    rows = 17
+    gs, ws = [], []
+    for r0, r1 in bands(h, count, rows):
+        want = o.render(w, h, spp, 6, rng=orng, rows=(r0, r1), threads=threads())
+        gs.append(got[r0:r1])
+        ws.append(want)
+    report(f"{cfg} {count} bands x {rows} rows of {w}x{h} {spp}spp", np.concatenate(gs), np.concatenate(ws),
+           {"rows": count * rows, "of_rows": h})
+
+
+def test_config4_full_frame_vs_reference_layout_tracer(rt):
+    """The whole 4-bunny frame: the production kernel (leaf trees, cooperative walks, pair
+    records) against the reference-layout tracer (the reference's own loop over the AoS arrays,
+    checked against the oracle in test_gpu_parity.py), same RNG."""
+    w, h = 1920, 1080
+    fast, frng = render_gpu(rt, "bunny4", w, h, 8, 6)
+    ref, rrng = render_gpu(rt, "bunny4", w, h, 8, 6, tracer="ref")
+    report("config4 full frame: production vs reference-layout tracer", fast, ref)
+    assert np.array_equal(frng, rrng)

@@ -6,18 +6,14 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 stop_if_fatal() { case "$1" in 124|134|137|139) echo "fatal exit $1 in $2"; exit "$1";; esac; }
 
-timeout -k 10 480 python -m pytest tests -q -m gpu -x > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -v -m gpu -x --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest -m gpu exit $rc"; tail -5 gpurun_out/pytest_gpu.log; stop_if_fatal $rc pytest
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 rc=$?; echo "smoke exit $rc"; tail -3 gpurun_out/smoke.log; stop_if_fatal $rc smoke
 timeout -k 10 300 python bench.py --steps ${BENCH_STEPS:-5} --warmup 2 ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench exit $rc"; tail -3 gpurun_out/bench.log; stop_if_fatal $rc bench
-if [ -n "${BENCH_AB:-}" ]; then
-  RT_FORCE_REFERENCE_LAYOUT=1 timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_ref.log 2>&1
-  rc=$?; echo "bench(ref layout) exit $rc"; tail -1 gpurun_out/bench_ref.log | cut -c1-400; stop_if_fatal $rc bench_ref
-fi
 if [ -n "${PROFILE:-}" ]; then
-  cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
+  cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-pmc > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
   rc=$?; echo "rocprof exit $rc"; cd "$GRAFT_REPO_ROOT"; stop_if_fatal $rc rocprof
 fi
 exit 0

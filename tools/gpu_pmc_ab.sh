@@ -1,5 +1,5 @@
 #!/bin/bash
-# One PMC pass per RT_TUNE value (render kernel instruction mix): AB="0 4096" bash tools/gpu_pmc_ab.sh
+# One PMC pass per --tune value (render kernel instruction mix): AB="0 4096" bash tools/gpu_pmc_ab.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -7,7 +7,7 @@ R="$PWD"
 CNT="${CNT:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SMEM}"
 for t in ${AB:-0}; do
   cd /tmp
-  RT_TUNE=$t timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $CNT --output-format csv -d "$R/gpurun_out/pmc_$t" -o run -- python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline > "$R/gpurun_out/pmc_$t.log" 2>&1
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $CNT --output-format csv -d "$R/gpurun_out/pmc_$t" -o run -- python3 "$R/bench.py" --tune $t --no-pmc --steps 1 --warmup 0 --no-cpu-baseline > "$R/gpurun_out/pmc_$t.log" 2>&1
   rc=$?; echo "pmc $t exit $rc"; cd "$R"; case $rc in 0) ;; *) exit $rc;; esac
   python3 - "$t" <<'PY'
 import csv, glob, sys, collections

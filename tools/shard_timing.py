@@ -1,15 +1,18 @@
-"""Per-rank render time of the multi-GPU split, measured on one GPU: the kernel for shard 0 of
-N (every N-th 16x16 tile) alone, for N = 1, 2, 4, 8 -- the compute side of strong scaling
-(the gather of N-1 shards into rank 0 and the unshard kernel come on top).  --weak: the frame
-grows with N as bench.py --scaling weak renders it (speedup = N x time(1) / time(N)).
+"""Per-rank render time of the multi-GPU split, measured on one GPU shard by shard: for N = 1, 2,
+4, 8 every shard of the frame's plan is rendered alone (its own RNG states, compact output) and
+timed with HIP events; the job's compute time is the slowest shard (the gather of N-1 shards into
+rank 0 and the unshard kernel come on top).  Plans: round-robin ("rr") and the bench's default
+cost plan ("cost": one probe frame's per-wave clocks, longest processing time first, heaviest
+tiles first on every rank).  --weak: the frame grows with N as bench.py --scaling weak renders it.
 
-    python tools/shard_timing.py [--config cfg2] [--reps 5] [--weak]
+    python tools/shard_timing.py [--config cfg2] [--reps 3] [--plans rr,cost] [--ns 1,2,4,8] [--weak]
 """
 import argparse
 import json
 import os
 import sys
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -18,39 +21,76 @@ import __graft_entry__ as G  # noqa: E402
 import bench  # noqa: E402
 
 
+def probe(rt, scene, W, H, SPP, BOUNCES):
+    """Per-tile cost of the whole frame from one production frame's per-wave clocks."""
+    lists, counts = rt.shard_plan(W, H, 1)
+    order = torch.from_numpy(lists[0, : counts[0]]).cuda()
+    rng = rt.alloc_rng(int(counts[0]) * 256)
+    rt.init_rng_tiles(rng, W, H, order, bench.SEED)
+    scene.upload(rng.data_ptr())
+    out = torch.zeros((int(counts[0]) * 256, 4), dtype=torch.float32, device="cuda")
+    clk = torch.zeros(int(counts[0]) * 4, dtype=torch.int64, device="cuda")
+    rt.render(scene, None, None, W, H, SPP, BOUNCES, 0, out_shard=out, tile_list=order, wave_clock=clk)
+    torch.cuda.synchronize()
+    cost = np.zeros(rt.sharding.tiles_total(W, H))
+    cost[lists[0, : counts[0]]] = clk.view(-1, 4).sum(1).double().cpu().numpy()
+    return cost
+
+
+def time_shard(rt, scene, W, H, SPP, BOUNCES, tiles, r, n, reps):
+    mine = torch.from_numpy(tiles).cuda()
+    rng = rt.alloc_rng(len(tiles) * 256)
+    rt.init_rng_tiles(rng, W, H, mine, bench.SEED)
+    scene.upload(rng.data_ptr())
+    bufs = [torch.zeros((len(tiles) * 256, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
+    ms = []
+    for i in range(reps + 1):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rt.render(scene, None, bufs[(i + 1) & 1], W, H, SPP, BOUNCES, i, r, n, out_shard=bufs[i & 1], tile_list=mine)
+        e1.record()
+        torch.cuda.synchronize()
+        if i:
+            ms.append(e0.elapsed_time(e1))
+    return float(np.mean(ms))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg2")
-    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--plans", default="rr,cost")
+    ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--weak", action="store_true", help="the frame grows with N as in bench.py --scaling weak")
     args = ap.parse_args()
     rt = G.load_package()
     scene_name, W0, H0, SPP, BOUNCES, _ = bench.CONFIGS[args.config]
     torch.cuda.set_device(0)
-    dev = torch.device("cuda", 0)
-    out = {}
-    for n in (1, 2, 4, 8):
-        W, H = bench.weak_size(W0, H0, n) if args.weak else (W0, H0)
-        scene = rt.Scene()
-        scene.setup(scene_name)
-        scene.set_viewport(W, H)
-        per = rt.shard_tiles(W, H, 0, n)
-        rng = rt.alloc_rng(per * 256)
-        rt.init_rng_states(rng, W, H, bench.SEED, 0, n)
-        scene.upload(rng.data_ptr())
-        bufs = [torch.zeros((per * 256, 4), dtype=torch.float32, device=dev) for _ in range(2)]
-        ms = []
-        for i in range(args.reps + 1):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            rt.render(scene, None, bufs[(i + 1) & 1], W, H, SPP, BOUNCES, i, 0, n, out_shard=bufs[i & 1])
-            e1.record()
-            torch.cuda.synchronize()
-            if i:
-                ms.append(e0.elapsed_time(e1))
-        out[n] = sum(ms) / len(ms)
-    res = {"config": args.config, "weak": args.weak, "shard0_ms": {str(k): round(v, 3) for k, v in out.items()},
-           "compute_speedup": {str(k): round((k if args.weak else 1) * out[1] / v, 2) for k, v in out.items()}}
+    res = {"config": args.config, "weak": args.weak, "plans": {}}
+    costs = {}
+    for plan in args.plans.split(","):
+        per_n = {}
+        for n in map(int, args.ns.split(",")):
+            W, H = bench.weak_size(W0, H0, n) if args.weak else (W0, H0)
+            scene = rt.Scene()
+            scene.setup(scene_name)
+            scene.set_viewport(W, H)
+            if plan == "cost":
+                if (W, H) not in costs:
+                    costs[(W, H)] = probe(rt, scene, W, H, SPP, BOUNCES)
+                lists, counts = rt.shard_plan(W, H, n, costs[(W, H)])
+            else:
+                lists, counts = rt.shard_plan(W, H, n)
+            shard_ms = [time_shard(rt, scene, W, H, SPP, BOUNCES, lists[r, : counts[r]], r, n, args.reps)
+                        for r in range(n)]
+            per_n[n] = shard_ms
+            print(json.dumps({"plan": plan, "n": n, "max_ms": round(max(shard_ms), 3),
+                              "shard_ms": [round(x, 3) for x in shard_ms]}), flush=True)
+        t1 = max(per_n[min(per_n)])
+        res["plans"][plan] = {"max_shard_ms": {str(n): round(max(v), 3) for n, v in per_n.items()},
+                              "shard_ms": {str(n): [round(x, 3) for x in v] for n, v in per_n.items()},
+                              "compute_speedup": {str(n): round((n if args.weak else 1) * t1 / max(v), 2)
+                                                  for n, v in per_n.items()}}
     print(json.dumps(res))
 
 

@@ -1,5 +1,4 @@
-"""Per-wave cost distribution of one frame (timing kernel, RT_TUNE=256+2048 must be set in the
-environment): start/end clocks of every 64-pixel wave, for load-balance analysis of the
+"""Per-wave cost distribution of one frame (timing kernel: bench --tune 256+2048 passed to rt_render): start/end clocks of every 64-pixel wave, for load-balance analysis of the
 multi-GPU split.  Records are indexed by workgroup (dispatch order); the sub-tile a workgroup
 renders is rt_kernel.hip xcd_block of that index.  Writes gpurun_out/wave_costs.npz and prints a summary."""
 import json
@@ -29,9 +28,9 @@ a, b = rt.alloc_surface(W, H), rt.alloc_surface(W, H)
 shard = torch.zeros((tiles * 256, 4), dtype=torch.float32, device="cuda")
 st = torch.zeros(24 + 8 * tiles * 4, dtype=torch.int64, device="cuda")
 if N > 1:
-    rt.render(scene, None, None, W, H, SPP, BOUNCES, 0, 0, N, out_shard=shard, stats=st)
+    rt.render(scene, None, None, W, H, SPP, BOUNCES, 0, 0, N, out_shard=shard, stats=st, tune=256 + 2048)
 else:
-    rt.render(scene, a, b, W, H, SPP, BOUNCES, 0, stats=st)
+    rt.render(scene, a, b, W, H, SPP, BOUNCES, 0, stats=st, tune=256 + 2048)
 torch.cuda.synchronize()
 v = st.cpu().numpy()
 t = v[24:].reshape(-1, 8)
