@@ -3,7 +3,9 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
 
-N = 1 runs BASELINE.json configs[1] (Stanford bunny scene, 1920x1080, 8 spp, 6 bounces).
+N = 1 runs BASELINE.json configs[1] (Stanford bunny scene, 1920x1080, 8 spp, 6 bounces), its 16x16
+tiles launched heaviest first (--plan cost: one untimed probe frame's per-wave clocks order them;
+the pixels, RNG layout and output are the reference's -- only the launch order changes).
 N > 1: one process per GPU.  Launched without a launcher (WORLD_SIZE unset), bench.py starts the
 N rank processes itself before touching the GPU and forwards rank 0's line; under
 torch.distributed.run it is one of the ranks.  The frame's 16x16 tiles are dealt over the ranks
@@ -296,6 +298,7 @@ def make_plan(rt, scene, W, H, SPP, BOUNCES, rank, world, plan_kind, dev):
     mine = torch.from_numpy(rr[rank, : rc[rank]]).to(dev)
     rng = rt.alloc_rng(int(rc[rank]) * 256)
     rt.init_rng_tiles(rng, W, H, mine, SEED)
+    scene.upload(rng.data_ptr())  # the probe's own states (the caller re-uploads with the run's)
     shard = torch.zeros((int(rc[rank]) * 256, 4), dtype=torch.float32, device=dev)
     clocks = torch.zeros(int(rc[rank]) * 4, dtype=torch.int64, device=dev)
     t0 = time.perf_counter()
@@ -562,13 +565,14 @@ def main():
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
                     help="N > 1: strong = the BASELINE frame split N ways; weak = sqrt(N) x resolution per axis")
     ap.add_argument("--plan", default=None, choices=["cost", "rr"],
-                    help="tile deal: cost (probe-frame clocks, longest first; default for N > 1) or round-robin")
+                    help="tile order / deal: cost (default: a probe frame's per-wave clocks, heaviest tiles first, "
+                         "longest-processing-time deal over ranks) or round-robin in row-major order")
     ap.add_argument("--tune", type=lambda s: int(s, 0), default=0, help="diagnostic A/B knobs (0 = production)")
     ap.add_argument("--check", action="store_true",
                     help="after timing, rank 0 re-renders the same frames unsharded and compares the final frame")
     args = ap.parse_args()
     if args.plan is None:
-        args.plan = "cost" if args.gpus > 1 else "rr"
+        args.plan = "cost"
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.pmc_child:
         return launch_ranks(args.gpus)
     return run(args)

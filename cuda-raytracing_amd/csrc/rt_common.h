@@ -71,7 +71,8 @@ __device__ __forceinline__ rtm::f3 ld3(const float* p) { return rtm::f3{p[0], p[
 // rt_shard_plan) or the round-robin deal t = shard_index + k * shard_count.  Entries < 0 are
 // padding (no pixels).
 __device__ __forceinline__ int shard_tile(const RenderArgs& a, int k) {
-    return a.tile_list ? a.tile_list[k] : a.shard_index + k * a.shard_count;
+    const int t = a.tile_list ? a.tile_list[k] : a.shard_index + k * a.shard_count;
+    return (t >= 0 && t < a.tiles_x * ((a.height + TILE - 1) / TILE)) ? t : -1;  // out of the frame: no pixels
 }
 
 // Tile-local pixel of tile-thread `tid` (0..255): wave w covers the 8x8 sub-tile

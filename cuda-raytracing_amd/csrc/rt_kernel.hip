@@ -49,6 +49,15 @@ static int check(hipError_t e, const char* what) {
 }
 
 extern "C" const char* rt_last_error(void) { return g_last_error.c_str(); }
+
+// Bytes of the device allocation holding p from p to its end (0 if p is not device memory).
+static size_t bytes_from(const void* p) {
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (!p || hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) != hipSuccess) return 0;
+    return size - (size_t)((const char*)p - (const char*)base);
+}
+
 void rt_internal_set_error(const char* msg) { set_error(msg); }
 
 // ---------------------------------------------------------------------------------------
@@ -732,10 +741,11 @@ __global__ __launch_bounds__(BLOCK) void init_rng_kernel(rt_rng_state* states, c
     } else {
         const int64_t k = s / BLOCK;
         const int tile = tile_list ? tile_list[k] : shard_index + (int)k * shard_count;
+        if (tile < 0 || tile >= tiles_x * ((height + TILE - 1) / TILE)) return;
         int lx, ly;
         tile_pixel((int)(s % BLOCK), &lx, &ly);
         const int x = (tile % tiles_x) * TILE + lx, y = (tile / tiles_x) * TILE + ly;
-        if (tile < 0 || x >= width || y >= height) return;
+        if (x >= width || y >= height) return;
         sub = (uint64_t)y * (uint64_t)width + (uint64_t)x;
     }
     uint32_t st[6];
@@ -921,12 +931,6 @@ __global__ __launch_bounds__(BLOCK) void fingerprint_kernel(HashArrays h, unsign
     if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);
 }
 
-static size_t bytes_from(const void* p) {
-    hipDeviceptr_t base = nullptr;
-    size_t size = 0;
-    if (!p || hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) != hipSuccess) return 0;
-    return size - (size_t)((const char*)p - (const char*)base);
-}
 
 static int foreign_mirror(const GPUScene* scene, hipStream_t st, MirrorDevice* out) {
     const size_t nb = bytes_from(scene->gpu_bvh_nodes), ni = bytes_from(scene->gpu_bvh_face_indices),
@@ -1023,6 +1027,25 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     a.wave_clock = (unsigned long long*)p->wave_clock;
     const int tiles = p->tile_list ? (int)p->tile_count : tiles_of_shard(p->width, p->height, p->shard_index, p->shard_count);
     if (tiles == 0) return 0;
+    // Every device buffer must cover what the launch touches: a short buffer would fault the GPU.
+    {
+        const bool compact = p->out_shard != nullptr;
+        const size_t slots = (size_t)tiles * TILE * TILE;
+        const size_t frame = (size_t)p->pitch * (size_t)(p->height - 1) + (size_t)p->width * 16;
+        const size_t rng_need = (compact ? slots : (size_t)p->width * p->height) * sizeof(rt_rng_state);
+        if (bytes_from(scene->rng_state) < rng_need) return set_error("rt_render: rng_state is smaller than the frame / shard");
+        if (compact && bytes_from(p->out_shard) < slots * 16) return set_error("rt_render: out_shard too small");
+        if (compact && p->surface_last_frame && bytes_from(p->surface_last_frame) < slots * 16)
+            return set_error("rt_render: surface_last_frame (shard) too small");
+        if (!compact && bytes_from(p->surface) < frame) return set_error("rt_render: surface too small");
+        if (!compact && p->surface_last_frame && bytes_from(p->surface_last_frame) < frame)
+            return set_error("rt_render: surface_last_frame too small");
+        if (p->tile_list && bytes_from(p->tile_list) < (size_t)tiles * 4) return set_error("rt_render: tile_list too small");
+        if (p->wave_clock && bytes_from(p->wave_clock) < (size_t)tiles * 4 * 8)
+            return set_error("rt_render: wave_clock too small");
+        const size_t stats_need = (RT_STAT_COUNT + ((p->tune & 2048u) ? (size_t)tiles * 4 * 8 : 0)) * 8;
+        if (p->stats && bytes_from(p->stats) < stats_need) return set_error("rt_render: stats too small");
+    }
     const bool want_ref = (p->flags & RT_RENDER_TRACER_REF) != 0;
     MirrorDevice mir;
     if ((!rt_internal_lookup_mirror(scene, &mir) || !mir.owned) && !want_ref) {
@@ -1070,6 +1093,7 @@ extern "C" int rt_init_rng(void* states, int width, int height, int shard_index,
         sc = shard_count;
     }
     if (count == 0) return 0;
+    if (bytes_from(states) < (size_t)count * sizeof(rt_rng_state)) return set_error("rt_init_rng: rng_states too small");
     const int blocks = (int)((count + BLOCK - 1) / BLOCK);
     hipLaunchKernelGGL(init_rng_kernel, dim3(blocks), dim3(BLOCK), 0, (hipStream_t)stream, (rt_rng_state*)states, jump,
                        seed, count, width, height, shard_index, sc, tiles_x, (const int32_t*)nullptr);
@@ -1083,6 +1107,8 @@ extern "C" int rt_init_rng_tiles(void* states, int width, int height, const int3
     const uint32_t* jump = device_jump_table();
     if (!jump) return set_error("rt_init_rng_tiles: jump table upload failed");
     const int64_t count = tile_count * BLOCK;
+    if (bytes_from(states) < (size_t)count * sizeof(rt_rng_state) || bytes_from(tile_list) < (size_t)tile_count * 4)
+        return set_error("rt_init_rng_tiles: rng_states or tile_list too small");
     hipLaunchKernelGGL(init_rng_kernel, dim3((unsigned)tile_count), dim3(BLOCK), 0, (hipStream_t)stream,
                        (rt_rng_state*)states, jump, seed, count, width, height, 0, 1, (width + TILE - 1) / TILE,
                        tile_list);
@@ -1091,7 +1117,11 @@ extern "C" int rt_init_rng_tiles(void* states, int width, int height, const int3
 
 extern "C" int rt_unshard(void* surface, uint64_t pitch, int width, int height, int shard_count, const void* shards,
                           int64_t per_shard, void* stream) {
-    if (!surface || !shards || shard_count <= 0 || per_shard <= 0) return set_error("rt_unshard: bad arguments");
+    if (!surface || !shards || shard_count <= 0 || per_shard <= 0 || width <= 0 || height <= 0)
+        return set_error("rt_unshard: bad arguments");
+    if (bytes_from(shards) < (size_t)shard_count * per_shard * BLOCK * 16 ||
+        bytes_from(surface) < pitch * (size_t)(height - 1) + (size_t)width * 16)
+        return set_error("rt_unshard: shards or surface too small");
     const int tiles_x = (width + TILE - 1) / TILE;
     hipLaunchKernelGGL(unshard_kernel, dim3((unsigned)per_shard, shard_count), dim3(BLOCK), 0, (hipStream_t)stream,
                        (char*)surface, pitch, width, height, shard_count, (const float4*)shards, per_shard, tiles_x,
@@ -1103,6 +1133,10 @@ extern "C" int rt_unshard_tiles(void* surface, uint64_t pitch, int width, int he
                                 const void* shards, int64_t per_shard, const int32_t* tile_lists, void* stream) {
     if (!surface || !shards || !tile_lists || shard_count <= 0 || per_shard <= 0 || width <= 0 || height <= 0)
         return set_error("rt_unshard_tiles: bad arguments");
+    if (bytes_from(shards) < (size_t)shard_count * per_shard * BLOCK * 16 ||
+        bytes_from(tile_lists) < (size_t)shard_count * per_shard * 4 ||
+        bytes_from(surface) < pitch * (size_t)(height - 1) + (size_t)width * 16)
+        return set_error("rt_unshard_tiles: shards, tile_lists or surface too small");
     hipLaunchKernelGGL(unshard_kernel, dim3((unsigned)per_shard, shard_count), dim3(BLOCK), 0, (hipStream_t)stream,
                        (char*)surface, pitch, width, height, shard_count, (const float4*)shards, per_shard,
                        (width + TILE - 1) / TILE, tile_lists);
@@ -1130,6 +1164,11 @@ extern "C" void raytracing_process(void* surface, void* surface_last_frame, int 
 extern "C" void init_rng(uint32_t thread_block_count, uint32_t thread_block_size, void* states, unsigned int seed) {
     const uint32_t* jump = device_jump_table();
     const int64_t count = (int64_t)thread_block_count * thread_block_size;
+    if (bytes_from(states) < (size_t)count * sizeof(rt_rng_state)) {
+        set_error("init_rng: rngStates is smaller than thread_block_count * thread_block_size states");
+        std::printf("(init_rng) failed: %s\n", rt_last_error());
+        return;
+    }
     if (!jump || count == 0) {
         set_error("init_rng: jump table upload failed");
         std::printf("(init_rng) failed: %s\n", rt_last_error());

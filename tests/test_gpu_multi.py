@@ -133,3 +133,27 @@ def test_bench_two_ranks_without_launcher(tmp_path):
     assert res["n_gpus"] == 2 and res["check_equal"] is True, res
     assert res["plan"]["kind"].startswith("cost") and sum(res["plan"]["tiles_per_rank"]) == 256
     assert len(res["rank_kernel_ms"]) == 2
+
+
+def test_short_buffers_are_refused(rt):
+    """rt_render / rt_init_rng_tiles / rt_unshard_tiles check every device buffer against what the
+    launch would touch and return an error instead of faulting the GPU.  (The check sees the
+    whole device allocation a pointer lies in -- torch's caching allocator hands out sub-blocks
+    of up to 2 MB segments -- so the frame here is large enough to overrun any segment.)"""
+    w, h = 1920, 1088
+    s = scene(rt, w, h)
+    small = rt.alloc_rng(256)  # one tile's states for an 8160-tile frame
+    s.upload(small.data_ptr())
+    a, b = rt.alloc_surface(w, h), rt.alloc_surface(w, h)
+    with pytest.raises(rt.RTError, match="rng_state"):
+        rt.render(s, a, b, w, h, 1, 1)
+    lists, counts = rt.shard_plan(w, h, 2)
+    mine = torch.from_numpy(lists[0, : counts[0]]).cuda()
+    with pytest.raises(rt.RTError):
+        rt.init_rng_tiles(small, w, h, mine, T.SEED)  # 4080 tiles into one tile's states
+    out = torch.zeros((256, 4), dtype=torch.float32, device="cuda")
+    with pytest.raises(rt.RTError, match="out_shard|rng_state"):
+        rt.render(s, None, None, w, h, 1, 1, 0, 0, 2, out_shard=out, tile_list=mine)
+    with pytest.raises(rt.RTError):
+        rt.unshard_tiles(a, w, h, torch.zeros((2, 256, 4), device="cuda"), torch.from_numpy(lists).cuda())
+    torch.cuda.synchronize()
