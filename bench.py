@@ -362,9 +362,19 @@ def run(args):
             tile_list = torch.from_numpy(lists[0, : int(counts[0])]).to(dev)
         rng = rt.alloc_rng(W * H)
         rt.init_rng_states(rng, W, H, SEED)
+        rng_init = rng.clone() if args.foreign else None
         bufs = [rt.alloc_surface(W, H) for _ in range(2)]
         pixels_rank = W * H
     scene.upload(rng.data_ptr())
+    target = scene
+    if args.foreign:
+        # the reference host's own Scene::Upload: its arrays in its own allocations, no mirror
+        # registered -- rendered through the fingerprint-gated path (rt_render, no host sync)
+        assert not sharded, "--foreign is a single-GPU measurement"
+        target = foreign_copy(rt, scene)
+        rt.render(target, bufs[0], bufs[1], W, H, SPP, BOUNCES, 0, tile_list=tile_list)  # first frame starts the build
+        rt.foreign_mirror_wait(target)
+        rng.copy_(rng_init)
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
 
@@ -373,7 +383,7 @@ def run(args):
             rt.render(scene, None, prev, W, H, SPP, BOUNCES, i, rank, world, out_shard=cur, tile_list=tile_list,
                       tune=args.tune, **kw)
         else:
-            rt.render(scene, cur, prev, W, H, SPP, BOUNCES, i, tile_list=tile_list, tune=args.tune, **kw)
+            rt.render(target, cur, prev, W, H, SPP, BOUNCES, i, tile_list=tile_list, tune=args.tune, **kw)
 
     if args.pmc_child:  # under rocprofv3 --pmc: a warm-up and two frames of the production kernel
         for i in range(3):
@@ -391,6 +401,8 @@ def run(args):
     stats0 = stats.cpu().numpy().astype(np.uint64)
     gpu = scene.gpu.contents
     bytes0 = algorithmic_bytes(stats0, gpu.sphere_count, pixels_rank)
+    if args.foreign and rt.foreign_last_tracer(target) != 1:
+        raise RuntimeError("--foreign: the production tracer did not render the frame")
 
     # --- the frame-end gather: rt_gather_shards (RCCL) unless rehearsing on gloo
     comm = None
@@ -513,6 +525,8 @@ def run(args):
             result["gather"] = gather_kind
         if not finite:  # (y, x) of non-finite pixels; the reference arithmetic can produce them too
             result["nonfinite_pixels"] = bad[:8].tolist()
+        if args.foreign:
+            result["config"]["scene_path"] = "foreign GPUScene (fingerprint-gated private mirror)"
         if args.check:
             result["check_equal"] = check_unsharded(rt, scene_name, W, H, SPP, BOUNCES, n_total, final)
         if world == 1 and not args.no_cpu_baseline:
@@ -526,6 +540,26 @@ def run(args):
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def foreign_copy(rt, scene):
+    """A GPUScene whose arrays are fresh exact-size device allocations (as the reference's
+    CUDA::DeviceMemory holds them) with the same contents: a scene this library never built."""
+    import ctypes
+
+    ha = scene.host_arrays()
+    g = scene.gpu.contents
+    f = rt.GPUScene()
+    ctypes.pointer(f)[0] = g
+    sizes = {"gpu_bvh_nodes": ha["nodes"].nbytes, "gpu_bvh_face_indices": ha["face_indices"].nbytes,
+             "gpu_vertices": ha["vertices"].nbytes, "gpu_faces": ha["faces"].nbytes,
+             "gpu_spheres": 32 * g.sphere_count, "gpu_materials": 64 * g.material_count}
+    for k, n in sizes.items():
+        p = ctypes.c_void_p()
+        if rt.lib().rt_malloc(ctypes.byref(p), n) or rt.lib().rt_memcpy_d2d(p, ctypes.c_void_p(getattr(g, k)), n):
+            raise RuntimeError(rt.lib().rt_last_error().decode())
+        setattr(f, k, p.value)
+    return f
 
 
 def check_unsharded(rt, scene_name, W, H, spp, bounces, frames, final):
@@ -568,6 +602,9 @@ def main():
                     help="tile order / deal: cost (default: a probe frame's per-wave clocks, heaviest tiles first, "
                          "longest-processing-time deal over ranks) or round-robin in row-major order")
     ap.add_argument("--tune", type=lambda s: int(s, 0), default=0, help="diagnostic A/B knobs (0 = production)")
+    ap.add_argument("--foreign", action="store_true",
+                    help="render a GPUScene filled outside this library (the reference's Scene::Upload pattern): "
+                         "fingerprint-gated mirror, no host synchronisation per frame")
     ap.add_argument("--check", action="store_true",
                     help="after timing, rank 0 re-renders the same frames unsharded and compares the final frame")
     args = ap.parse_args()

@@ -78,6 +78,8 @@ SIGNATURES = {
     "raytracing_process": (None, [_P, _P, _I, _I, _SZ, _I, _P]),
     "init_rng": (None, [_U32, _U32, _P, ctypes.c_uint]),
     "rt_render": (_I, [ctypes.POINTER(RenderParams), _P, _P]),
+    "rt_foreign_mirror_wait": (_I, [_P]),
+    "rt_foreign_last_tracer": (_I, [_P]),
     "rt_init_rng": (_I, [_P, _I, _I, _I, _I, _U32, _P]),
     "rt_shard_tiles": (ctypes.c_int64, [_I, _I, _I, _I]),
     "rt_unshard": (_I, [_P, _U64, _I, _I, _I, _P, ctypes.c_int64, _P]),
@@ -356,6 +358,18 @@ def render(scene, surface, last, width, height, spp, bounces, frame_index=0, sha
         p.stats = stats.data_ptr()
     gpu = scene.gpu if hasattr(scene, "gpu") else ctypes.pointer(scene)  # Scene, or a GPUScene filled by the caller
     _check(lib().rt_render(ctypes.byref(p), ctypes.cast(gpu, ctypes.c_void_p), _stream_ptr(stream)), "rt_render")
+
+
+def foreign_mirror_wait(gpu_scene):
+    """rt_foreign_mirror_wait: block until the background mirror build of a foreign GPUScene (a
+    ctypes GPUScene filled by the caller) has finished; the next render installs it."""
+    _check(lib().rt_foreign_mirror_wait(ctypes.byref(gpu_scene)), "rt_foreign_mirror_wait")
+
+
+def foreign_last_tracer(gpu_scene):
+    """rt_foreign_last_tracer: 1 production tracer, 0 reference layout (fingerprint mismatch),
+    -1 no mirror yet (test diagnostics; synchronises the device)."""
+    return int(lib().rt_foreign_last_tracer(ctypes.byref(gpu_scene)))
 
 
 def cluster_cull_host(origin, nd, best, node):

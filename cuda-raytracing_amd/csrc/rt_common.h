@@ -42,6 +42,8 @@ struct RenderArgs {
     int shard_index, shard_count, tiles_x;
     const int32_t* tile_list;        // tile of list entry k (rt_render_params.tile_list) or null: round-robin
     unsigned long long* wave_clock;  // per-wave elapsed clock ticks, [list entry][4 sub-tiles], or null
+    const int* gate;                 // foreign scenes: the kernel runs only if *gate == gate_value
+    int gate_value;
     unsigned long long* stats;
     unsigned long long* seg_counter;
     int scene_fast;  // all node bounds inside the filtered-slab range (rt_fast.h)

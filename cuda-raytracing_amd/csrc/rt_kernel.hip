@@ -19,8 +19,12 @@
 #include <vector>
 #include <cstring>
 #include <map>
+#include <atomic>
+#include <memory>
 #include <mutex>
+#include <stdexcept>
 #include <string>
+#include <thread>
 
 #include "rt_abi.h"
 #include "rt_device.h"
@@ -404,6 +408,7 @@ __device__ __forceinline__ void shade_pixel(const RenderArgs& a, uint32_t* stk, 
 // balances cheap (sky) against expensive (floor leaf) tiles.
 template <class Tracer, int STACK, bool STATS>
 __global__ __launch_bounds__(WAVE) void render_kernel(RenderArgs a) {
+    if (a.gate && *a.gate != a.gate_value) return;  // foreign scenes: the other tracer renders this frame
     __shared__ uint32_t stack_lds[STACK * Tracer::WORDS * WAVE];
     uint32_t* const stk = stack_lds + threadIdx.x;
     const int g = (int)blockIdx.x;
@@ -527,6 +532,7 @@ __device__ __forceinline__ int xcd_block(uint32_t tune) {
 // done.  The per-pixel draw order (u, v, then 4 draws per hit) is the reference's.
 template <int STACK, bool STATS, int MODE>
 __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* const stk, uint32_t* const scratch) {
+    if (a.gate && *a.gate != a.gate_value) return;  // foreign scenes: the other tracer renders this frame
     const float4* nodes4 = reinterpret_cast<const float4*>(a.nodes);
     const float4* tris = reinterpret_cast<const float4*>(a.tris);
     // one 64-lane workgroup per 8x8 sub-tile: tile k = lb / 4, sub-tile lb % 4
@@ -900,11 +906,22 @@ extern "C" int64_t rt_shard_tiles(int width, int height, int shard_index, int sh
 
 // ---------------------------------------------------------------------------------------
 // Foreign scenes.  A GPUScene filled by another host (the reference's own Scene::Upload,
-// Scene.cpp:182-234) never registers a mirror.  On first use the arrays are read back, the
-// mirror is built exactly as rt_scene_upload builds it, and it is kept with a content
-// fingerprint of the four arrays; every later call re-hashes them on the GPU (~15 MB, a few
-// microseconds plus one 8-byte read-back) and rebuilds when they changed -- Scene::Upload
-// replaces buffers whose addresses the allocator may hand out again.
+// Scene.cpp:182-234) never registers a mirror.  raytracing_process keeps the reference's
+// asynchronous contract (main_raytracing.cu:202-220): no call waits for the device.
+//
+//   * Every frame enqueues, on the render stream, a content fingerprint of the four arrays the
+//     mirror derives from (~15 MB read, a few microseconds) and a one-thread kernel that sets a
+//     device flag: 1 when it equals the fingerprint of the installed mirror.  The production
+//     kernel is launched gated on flag == 1 and the reference-layout tracer (which reads the AoS
+//     arrays directly, no mirror) gated on flag == 0: exactly one of them renders the frame, and
+//     the other's waves exit at their first instruction.
+//   * The fingerprint is also copied (async) to pinned host memory.  A later call that finds it
+//     different from the installed mirror's -- or a first call, with no mirror yet -- starts a
+//     rebuild: async copies of the arrays to pinned host buffers, then a worker thread waits for
+//     them, builds the mirror exactly as rt_scene_upload does, uploads it on its own stream and
+//     hands it over; the next call installs it.  Until then frames render through the reference
+//     layout, bit-identical by construction.
+//   * A replaced mirror is freed stream-ordered after the frames that may still read it.
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
     x ^= x >> 30;
@@ -931,49 +948,248 @@ __global__ __launch_bounds__(BLOCK) void fingerprint_kernel(HashArrays h, unsign
     if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);
 }
 
+// flag = (fingerprint == expected) for the gated launches; then clears the accumulator for the
+// next frame (kernels on one stream run in order).
+__global__ void fingerprint_gate_kernel(unsigned long long* acc, unsigned long long salt, unsigned long long expected,
+                                        int have, int* flag, unsigned long long* out) {
+    const unsigned long long fp = *acc ^ salt;
+    *flag = (have && fp == expected) ? 1 : 0;
+    *out = fp;
+    *acc = 0;
+}
 
-static int foreign_mirror(const GPUScene* scene, hipStream_t st, MirrorDevice* out) {
-    const size_t nb = bytes_from(scene->gpu_bvh_nodes), ni = bytes_from(scene->gpu_bvh_face_indices),
-                 nf = bytes_from(scene->gpu_faces), nv = bytes_from(scene->gpu_vertices);
-    if (!nb || !ni || !nf || !nv) return set_error("rt_render: scene arrays are not device allocations");
-    static unsigned long long* d_hash = nullptr;
-    static unsigned long long* h_hash = nullptr;
-    if (!d_hash && (hipMalloc(&d_hash, 8) != hipSuccess || hipHostMalloc(&h_hash, 8) != hipSuccess))
-        return set_error("rt_render: fingerprint buffers");
+static uint64_t host_fingerprint(const std::vector<const uint32_t*>& w, const std::vector<size_t>& n, uint64_t salt) {
+    auto mix = [](unsigned long long x) {
+        x ^= x >> 30;
+        x *= 0xbf58476d1ce4e5b9ull;
+        x ^= x >> 27;
+        x *= 0x94d049bb133111ebull;
+        x ^= x >> 31;
+        return x;
+    };
+    unsigned long long acc = 0;
+    for (int k = 0; k < 4; k++)
+        for (size_t i = 0; i < n[k]; i++) acc += mix(((unsigned long long)k << 60) ^ ((unsigned long long)i << 32) ^ w[k][i]);
+    return acc ^ salt;
+}
+
+namespace {
+struct ForeignBuild {  // one background rebuild
+    std::thread worker;
+    std::atomic<int> state{0};  // 1 running, 2 done (ok), 3 failed
+    std::vector<char> host[4];
+    char* pinned[4] = {nullptr, nullptr, nullptr, nullptr};
+    size_t bytes[4] = {0, 0, 0, 0};
+    hipEvent_t copied = nullptr;
+    uint64_t fingerprint = 0;
+    void* block = nullptr;
+    MirrorDevice dev;
+    std::string error;
+    ~ForeignBuild() {
+        if (worker.joinable()) worker.join();
+    }
+};
+
+struct ForeignEntry {
+    int device = 0;
+    unsigned long long* d_acc = nullptr;  // fingerprint accumulator, fingerprint of the frame
+    unsigned long long* d_fp = nullptr;
+    int* d_flag = nullptr;
+    unsigned long long* h_fp = nullptr;   // pinned copy of the last fingerprint
+    hipEvent_t fp_ready = nullptr;
+    bool fp_pending = false;
+    bool have = false;      // a mirror is installed
+    uint64_t fp_mirror = 0;  // fingerprint of the arrays it was built from
+    MirrorDevice dev;
+    void* block = nullptr;
+    std::unique_ptr<ForeignBuild> build;
+    std::vector<void*> retired;  // freed stream-ordered at the next call
+};
+
+std::mutex g_foreign_mutex;
+std::map<const void*, std::unique_ptr<ForeignEntry>> g_foreign;  // keyed by the BVH node array
+
+void upload_mirror(ForeignBuild* b) {
+    try {
+        const GPUBVHNode* nodes = reinterpret_cast<const GPUBVHNode*>(b->pinned[0]);
+        const uint32_t* fi = reinterpret_cast<const uint32_t*>(b->pinned[1]);
+        const GPUFace* faces = reinterpret_cast<const GPUFace*>(b->pinned[2]);
+        const GPUVertex* verts = reinterpret_cast<const GPUVertex*>(b->pinned[3]);
+        if (hipEventSynchronize(b->copied) != hipSuccess) throw std::runtime_error("array read-back failed");
+        const std::vector<const uint32_t*> w = {(const uint32_t*)nodes, fi, (const uint32_t*)faces, (const uint32_t*)verts};
+        const std::vector<size_t> n = {b->bytes[0] / 4, b->bytes[1] / 4, b->bytes[2] / 4, b->bytes[3] / 4};
+        b->fingerprint = host_fingerprint(w, n, (unsigned long long)b->bytes[0] << 1 ^ (unsigned long long)b->bytes[3] << 33);
+        MirrorHost mh;
+        rt_build_mirror(nodes, b->bytes[0] / sizeof(GPUBVHNode), fi, b->bytes[1] / 4, faces, b->bytes[2] / sizeof(GPUFace),
+                        verts, b->bytes[3] / sizeof(GPUVertex), &mh);
+        const std::vector<float>* parts[6] = {&mh.tris, &mh.pairs, &mh.tree, &mh.ltris, &mh.spairs, &mh.flat};
+        size_t total = 64;
+        for (auto* v : parts) total += v->size() * 4;
+        hipStream_t st;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) throw std::runtime_error("stream");
+        void* block = nullptr;
+        if (hipMallocAsync(&block, total, st) != hipSuccess) throw std::runtime_error("mirror allocation failed");
+        char* p = static_cast<char*>(block);
+        const void* where[6];
+        for (int i = 0; i < 6; i++) {
+            const size_t nb = parts[i]->size() * 4;
+            where[i] = nb ? p : nullptr;
+            if (nb && hipMemcpyAsync(p, parts[i]->data(), nb, hipMemcpyHostToDevice, st) != hipSuccess)
+                throw std::runtime_error("mirror upload failed");
+            p += nb;
+        }
+        const hipError_t e = hipStreamSynchronize(st);  // this worker thread only
+        hipStreamDestroy(st);
+        if (e != hipSuccess) throw std::runtime_error("mirror upload failed");
+        b->block = block;
+        b->dev.tris = where[0], b->dev.pairs = where[1], b->dev.tree = where[2], b->dev.ltris = where[3];
+        b->dev.spairs = where[4], b->dev.flat = where[5];
+        b->dev.depth = mh.depth, b->dev.fast = mh.fast, b->dev.owned = false, b->dev.fingerprint = b->fingerprint;
+        b->state = 2;
+    } catch (const std::exception& e) {
+        b->error = e.what();
+        b->state = 3;
+    }
+}
+
+void free_build(ForeignBuild* b) {
+    if (b->worker.joinable()) b->worker.join();
+    for (auto* p : b->pinned)
+        if (p) hipHostFree(p);
+    if (b->copied) hipEventDestroy(b->copied);
+}
+
+// Start a rebuild from the arrays as they are on `st` now.
+int start_build(ForeignEntry& fe, const GPUScene* scene, hipStream_t st, const size_t bytes[4]) {
+    auto b = std::make_unique<ForeignBuild>();
+    const void* src[4] = {scene->gpu_bvh_nodes, scene->gpu_bvh_face_indices, scene->gpu_faces, scene->gpu_vertices};
+    for (int i = 0; i < 4; i++) {
+        b->bytes[i] = bytes[i];
+        if (hipHostMalloc((void**)&b->pinned[i], bytes[i] ? bytes[i] : 16) != hipSuccess ||
+            hipMemcpyAsync(b->pinned[i], src[i], bytes[i], hipMemcpyDeviceToHost, st) != hipSuccess) {
+            free_build(b.get());
+            return set_error("rt_render: foreign scene read-back failed");
+        }
+    }
+    if (hipEventCreateWithFlags(&b->copied, hipEventDisableTiming) != hipSuccess || hipEventRecord(b->copied, st) != hipSuccess) {
+        free_build(b.get());
+        return set_error("rt_render: foreign scene event");
+    }
+    b->state = 1;
+    ForeignBuild* raw = b.get();
+    b->worker = std::thread([raw, dev = fe.device]() {
+        hipSetDevice(dev);
+        upload_mirror(raw);
+    });
+    fe.build = std::move(b);
+    return 0;
+}
+
+ForeignEntry* foreign_entry(const GPUScene* scene) {
+    std::lock_guard<std::mutex> lock(g_foreign_mutex);
+    auto& slot = g_foreign[scene->gpu_bvh_nodes];
+    if (!slot) {
+        auto fe = std::make_unique<ForeignEntry>();
+        hipGetDevice(&fe->device);
+        if (hipMalloc(&fe->d_acc, 16) != hipSuccess || hipMalloc(&fe->d_fp, 8) != hipSuccess ||
+            hipMalloc(&fe->d_flag, 4) != hipSuccess || hipMemset(fe->d_acc, 0, 16) != hipSuccess ||
+            hipHostMalloc((void**)&fe->h_fp, 8) != hipSuccess ||
+            hipEventCreateWithFlags(&fe->fp_ready, hipEventDisableTiming) != hipSuccess) {
+            set_error("rt_render: foreign scene state");
+            return nullptr;
+        }
+        slot = std::move(fe);
+    }
+    return slot.get();
+}
+}  // namespace
+
+// Per frame for a foreign scene: install a finished rebuild, enqueue the fingerprint gate,
+// start a rebuild when the arrays no longer match.  *mir receives the installed mirror (if any);
+// *gate the device flag the two launches are gated on.
+static int foreign_frame(const GPUScene* scene, hipStream_t st, MirrorDevice* mir, bool* have, int** gate) {
+    const size_t bytes[4] = {bytes_from(scene->gpu_bvh_nodes), bytes_from(scene->gpu_bvh_face_indices),
+                             bytes_from(scene->gpu_faces), bytes_from(scene->gpu_vertices)};
+    if (!bytes[0] || !bytes[1] || !bytes[2] || !bytes[3]) return set_error("rt_render: scene arrays are not device allocations");
+    ForeignEntry* fe = foreign_entry(scene);
+    if (!fe) return 1;
+    for (void* p : fe->retired) hipFreeAsync(p, st);  // after every frame already enqueued
+    fe->retired.clear();
+    if (fe->build && fe->build->state >= 2) {
+        ForeignBuild* b = fe->build.get();
+        if (b->worker.joinable()) b->worker.join();
+        if (b->state == 2) {
+            if (fe->block) fe->retired.push_back(fe->block);
+            fe->block = b->block;
+            fe->dev = b->dev;
+            fe->fp_mirror = b->fingerprint;
+            fe->have = true;
+        }
+        free_build(b);
+        fe->build.reset();
+    }
+    const unsigned long long salt = (unsigned long long)bytes[0] << 1 ^ (unsigned long long)bytes[3] << 33;
+    // the previous frame's fingerprint, if it has landed: a mismatch starts a rebuild
+    bool stale = !fe->have;
+    if (fe->fp_pending && hipEventQuery(fe->fp_ready) == hipSuccess) {
+        fe->fp_pending = false;
+        stale = stale || *fe->h_fp != fe->fp_mirror;
+    }
+    if (stale && !fe->build && start_build(*fe, scene, st, bytes) != 0) return 1;
     HashArrays h;
-    h.w[0] = (const uint32_t*)scene->gpu_bvh_nodes, h.n[0] = nb / 4;
-    h.w[1] = scene->gpu_bvh_face_indices, h.n[1] = ni / 4;
-    h.w[2] = (const uint32_t*)scene->gpu_faces, h.n[2] = nf / 4;
-    h.w[3] = (const uint32_t*)scene->gpu_vertices, h.n[3] = nv / 4;
-    if (hipMemsetAsync(d_hash, 0, 8, st) != hipSuccess) return set_error("rt_render: fingerprint");
-    hipLaunchKernelGGL(fingerprint_kernel, dim3(1024), dim3(BLOCK), 0, st, h, d_hash);
-    if (hipMemcpyAsync(h_hash, d_hash, 8, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
-        return set_error("rt_render: fingerprint");
-    const unsigned long long fp = *h_hash ^ ((unsigned long long)nb << 1) ^ ((unsigned long long)nv << 33);
-    MirrorDevice m;
-    if (rt_internal_lookup_mirror(scene, &m) && !m.owned && m.fingerprint == fp) {
-        *out = m;
+    h.w[0] = (const uint32_t*)scene->gpu_bvh_nodes, h.n[0] = bytes[0] / 4;
+    h.w[1] = scene->gpu_bvh_face_indices, h.n[1] = bytes[1] / 4;
+    h.w[2] = (const uint32_t*)scene->gpu_faces, h.n[2] = bytes[2] / 4;
+    h.w[3] = (const uint32_t*)scene->gpu_vertices, h.n[3] = bytes[3] / 4;
+    hipLaunchKernelGGL(fingerprint_kernel, dim3(1024), dim3(BLOCK), 0, st, h, fe->d_acc);
+    hipLaunchKernelGGL(fingerprint_gate_kernel, dim3(1), dim3(1), 0, st, fe->d_acc, salt, (unsigned long long)fe->fp_mirror,
+                       fe->have ? 1 : 0, fe->d_flag, fe->d_fp);
+    if (!fe->fp_pending) {
+        if (hipMemcpyAsync(fe->h_fp, fe->d_fp, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipEventRecord(fe->fp_ready, st) != hipSuccess)
+            return set_error("rt_render: fingerprint read-back");
+        fe->fp_pending = true;
+    }
+    if (hipGetLastError() != hipSuccess) return set_error("rt_render: fingerprint launch");
+    *have = fe->have;
+    *mir = fe->dev;
+    *gate = fe->d_flag;
+    return 0;
+}
+
+// Tests: which tracer rendered this foreign scene's last frame -- 1 the production tracer (its
+// mirror matched the frame's fingerprint), 0 the reference layout (mismatch), -1 no mirror was
+// installed (reference layout, ungated).  Synchronises the device.
+extern "C" int rt_foreign_last_tracer(const GPUScene* scene) {
+    ForeignEntry* fe = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(g_foreign_mutex);
+        auto it = g_foreign.find(scene->gpu_bvh_nodes);
+        if (it == g_foreign.end()) return -2;
+        fe = it->second.get();
+    }
+    if (!fe->have) return -1;
+    int flag = -3;
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&flag, fe->d_flag, 4, hipMemcpyDeviceToHost) != hipSuccess) return -3;
+    return flag;
+}
+
+// Tests and benchmarks: wait (host) until a rebuild for this foreign scene has finished, then let
+// the next frame install it.  Returns 0 when a mirror is or will be installed, 1 on failure.
+extern "C" int rt_foreign_mirror_wait(const GPUScene* scene) {
+    ForeignEntry* fe = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(g_foreign_mutex);
+        auto it = g_foreign.find(scene->gpu_bvh_nodes);
+        if (it == g_foreign.end()) return set_error("rt_foreign_mirror_wait: scene never rendered");
+        fe = it->second.get();
+    }
+    if (fe->build) {
+        if (fe->build->worker.joinable()) fe->build->worker.join();
+        if (fe->build->state != 2) return set_error(std::string("rt_foreign_mirror_wait: ") + fe->build->error);
         return 0;
     }
-    std::vector<GPUBVHNode> nodes(nb / sizeof(GPUBVHNode));
-    std::vector<uint32_t> fi(ni / 4);
-    std::vector<GPUFace> faces(nf / sizeof(GPUFace));
-    std::vector<GPUVertex> verts(nv / sizeof(GPUVertex));
-    if (hipMemcpy(nodes.data(), scene->gpu_bvh_nodes, nodes.size() * sizeof(GPUBVHNode), hipMemcpyDeviceToHost) ||
-        hipMemcpy(fi.data(), scene->gpu_bvh_face_indices, fi.size() * 4, hipMemcpyDeviceToHost) ||
-        hipMemcpy(faces.data(), scene->gpu_faces, faces.size() * sizeof(GPUFace), hipMemcpyDeviceToHost) ||
-        hipMemcpy(verts.data(), scene->gpu_vertices, verts.size() * sizeof(GPUVertex), hipMemcpyDeviceToHost))
-        return set_error("rt_render: reading back the scene arrays failed");
-    MirrorHost mh;
-    try {
-        rt_build_mirror(nodes.data(), nodes.size(), fi.data(), fi.size(), faces.data(), faces.size(), verts.data(),
-                        verts.size(), &mh);
-    } catch (const std::exception& e) {
-        return set_error(std::string("rt_render: ") + e.what());
-    }
-    if (rt_internal_install_mirror(scene, mh, false, fp) != 0) return 1;
-    if (!rt_internal_lookup_mirror(scene, out)) return set_error("rt_render: mirror registry");
-    return 0;
+    return fe->have ? 0 : set_error("rt_foreign_mirror_wait: no mirror");
 }
 
 // Per-configuration wave-cost history for the priority scheme in render_fast_body: one uint32
@@ -1048,9 +1264,12 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     }
     const bool want_ref = (p->flags & RT_RENDER_TRACER_REF) != 0;
     MirrorDevice mir;
+    int* gate = nullptr;  // foreign scenes: device flag selecting production (1) or reference-layout (0) tracer
+    bool foreign_fast = false;
     if ((!rt_internal_lookup_mirror(scene, &mir) || !mir.owned) && !want_ref) {
-        // not uploaded through rt_scene_upload: build / revalidate a private mirror
-        if (foreign_mirror(scene, (hipStream_t)stream, &mir) != 0) return 1;
+        // not uploaded through rt_scene_upload: fingerprint-gated private mirror, no host sync
+        if (foreign_frame(scene, (hipStream_t)stream, &mir, &foreign_fast, &gate) != 0) return 1;
+        if (!foreign_fast) gate = nullptr, mir = MirrorDevice{};  // no mirror yet: reference layout, ungated
     }
     const void* tris = mir.tris;
     const int depth = mir.depth;
@@ -1067,7 +1286,15 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     const bool want_flat = (p->flags & RT_RENDER_TRACER_FLAT) != 0;
     a.scene_fast = scene_fast ? 1 : 0;
     hipError_t e;
-    if (!a.tris)
+    if (gate) {  // foreign scene with a mirror: exactly one of the two runs, by the frame's fingerprint
+        a.gate = gate, a.gate_value = 1;
+        e = want_flat ? launch_variant<FlatTracer>(a, tiles * 4, depth, stats, s) : launch_fast(a, tiles, depth, stats, s);
+        if (e == hipSuccess) {
+            RenderArgs r = a;
+            r.tris = nullptr, r.gate_value = 0;
+            e = launch_variant<RefTracer>(r, tiles * 4, -1, stats, s);
+        }
+    } else if (!a.tris)
         e = launch_variant<RefTracer>(a, tiles * 4, depth, stats, s);
     else if (want_flat)
         e = launch_variant<FlatTracer>(a, tiles * 4, depth, stats, s);

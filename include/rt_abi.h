@@ -215,8 +215,18 @@ enum {
     RT_STAT_COUNT = 24
 };
 
-/* Render on `stream` (a hipStream_t, NULL = null stream).  Returns 0 or an error code. */
+/* Render on `stream` (a hipStream_t, NULL = null stream).  Returns 0 or an error code.
+ * A GPUScene filled by another host (the reference's own Scene::Upload) is rendered without any
+ * host synchronisation: each frame's arrays are fingerprinted on the device, and the frame runs the
+ * production tracer when a private mirror built from exactly those arrays is installed, the
+ * reference-layout tracer otherwise, while a worker thread (re)builds the mirror in the background. */
 int rt_render(const rt_render_params* params, const GPUScene* scene, void* stream);
+/* Foreign scenes: block until the background mirror build started by the last rt_render of this
+ * scene has finished (the next rt_render installs it).  For tests and benchmarks; 0 or an error. */
+int rt_foreign_mirror_wait(const GPUScene* scene);
+/* Foreign scenes, for tests: the tracer of the last frame -- 1 production (mirror matched the
+ * frame's fingerprint), 0 reference layout (mismatch), -1 no mirror installed yet.  Synchronises. */
+int rt_foreign_last_tracer(const GPUScene* scene);
 
 /* init_rng for the pixels of one shard: state index s of shard (shard_index, shard_count)
  * of a width x height frame gets curand_init(seed, pixel_id(s), 0).  With shard_count == 1

@@ -210,8 +210,10 @@ def _dev_copy(rt, src_ptr, nbytes):
 
 def test_foreign_gpuscene(rt):
     """A GPUScene filled by another host (the reference's own Scene::Upload) -- no mirror was
-    registered for it: the fast path builds one on first use, equals the registered path, and
-    notices when the arrays change in place (revalidated by content fingerprint)."""
+    registered for it.  No call waits for the device: the first frames render through the
+    reference layout while a worker thread builds the mirror; once installed, frames whose arrays
+    match its fingerprint run the production tracer; an in-place change of the arrays is caught by
+    the device-side fingerprint of that very frame (reference layout again) and rebuilt."""
     import ctypes
     w, h = 64, 36
     s = make_scene(rt, "bunny", w, h)
@@ -242,18 +244,29 @@ def test_foreign_gpuscene(rt):
 
         ref = frame(s, rng)
         assert np.array_equal(frame(f, frng), ref)
-        assert np.array_equal(frame(f, frng), ref)  # cached mirror, fingerprint unchanged
-        # move every vertex in place (same buffer, same size): the mirror must follow
+        assert rt.foreign_last_tracer(f) == -1  # no mirror yet: reference layout
+        rt.foreign_mirror_wait(f)
+        assert np.array_equal(frame(f, frng), ref)  # installs the mirror, fingerprint matches
+        assert rt.foreign_last_tracer(f) == 1
+        assert np.array_equal(frame(f, frng), ref)
+        assert rt.foreign_last_tracer(f) == 1
+        # move every vertex in place (same buffer, same size): this very frame must notice
         vert = ha["vertices"].copy().view(np.float32).reshape(-1, 8)
         vert[:, 0] += np.float32(0.75)
         src = torch.from_numpy(vert.reshape(-1).copy()).cuda()
         assert rt.lib().rt_memcpy_d2d(owned["gpu_vertices"], ctypes.c_void_p(src.data_ptr()), vert.nbytes) == 0
         torch.cuda.synchronize()
-        moved_fast = frame(f, frng)
         moved_ref = frame(f, frng, tracer="ref")
-        assert not np.array_equal(moved_fast, ref)
-        assert np.array_equal(moved_fast, moved_ref)
+        moved = frame(f, frng)
+        assert rt.foreign_last_tracer(f) == 0  # stale mirror: the reference layout rendered it
+        assert not np.array_equal(moved, ref)
+        assert np.array_equal(moved, moved_ref)
+        frame(f, frng)  # the mismatch has reached the host: a rebuild starts
+        rt.foreign_mirror_wait(f)
+        assert np.array_equal(frame(f, frng), moved_ref)
+        assert rt.foreign_last_tracer(f) == 1  # rebuilt mirror in use
     finally:
+        torch.cuda.synchronize()
         for p in owned.values():
             rt.lib().rt_free(p)
 
