@@ -204,8 +204,12 @@ def pmc_pass(args, out_dir, timeout_s=150):
                                env=dict(os.environ, TMPDIR=tempfile.gettempdir()))
         except subprocess.TimeoutExpired:
             return None, f"pass {i} timed out"
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "child.log"), "w") as fh:
+            fh.write(r.stdout + "\n---- stderr ----\n" + r.stderr)
         if r.returncode != 0:
-            return None, f"pass {i} exit {r.returncode}: {r.stderr[-300:]}"
+            err = [l for l in r.stderr.splitlines() if "Error" in l or "error" in l or "Traceback" in l]
+            return None, f"pass {i} exit {r.returncode}: {' | '.join(err[-3:])[-400:]}"
         vals = {}
         for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for row in csv.DictReader(open(path)):
