@@ -321,6 +321,25 @@ def make_plan(rt, scene, W, H, SPP, BOUNCES, rank, world, plan_kind, dev):
     return lists, counts, {"probe_frame_s": round(probe_s, 4), "kind": "cost (probe-frame wave clocks, LPT)"}
 
 
+def make_lane_map(rt, render, rng, slots, units, dev):
+    """rt_lane_plan for this rank's list: one probe frame of per-pixel work (timing variant of the
+    production kernel, set-up, untimed) on a copy of the RNG states, then the split plan.
+    Returns (device int32 lane map, info)."""
+    import torch
+
+    rng_saved = rng.clone()
+    cost = torch.zeros(slots, dtype=torch.int32, device=dev)  # one per slot of the tile list
+    t0 = time.perf_counter()
+    render(cost)
+    torch.cuda.synchronize()
+    probe_s = time.perf_counter() - t0
+    rng.copy_(rng_saved)
+    del rng_saved
+    lm, nlong = rt.lane_plan(cost.cpu().numpy(), units, 1.0)
+    return torch.from_numpy(lm).to(dev), {"lane_probe_s": round(probe_s, 4), "waves": int(lm.size // 64),
+                                          "long_waves": nlong, "parallel_units": units}
+
+
 def run(args):
     import torch
     import torch.distributed as dist
@@ -382,12 +401,24 @@ def run(args):
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
 
+    lane_slots = None
+
     def render(i, cur, prev, **kw):
         if sharded:
             rt.render(scene, None, prev, W, H, SPP, BOUNCES, i, rank, world, out_shard=cur, tile_list=tile_list,
-                      tune=args.tune, **kw)
+                      tune=args.tune, lane_slots=lane_slots, **kw)
         else:
-            rt.render(target, cur, prev, W, H, SPP, BOUNCES, i, tile_list=tile_list, tune=args.tune, **kw)
+            rt.render(target, cur, prev, W, H, SPP, BOUNCES, i, tile_list=tile_list, tune=args.tune,
+                      lane_slots=lane_slots, **kw)
+
+    # lane plan (rt_lane_plan): split the waves whose pixels form the frame's serial tail
+    lanes_on = args.lanes == "on" or (args.lanes == "auto" and sharded)
+    if lanes_on and not args.foreign and tile_list is not None:
+        t1 = time.perf_counter()
+        lane_slots, lane_info = make_lane_map(rt, lambda cost: render(0, bufs[0], None, lane_cost=cost), rng,
+                                              tile_list.numel() * 256, args.lane_units, dev)
+        setup_s += time.perf_counter() - t1
+        plan_info = dict(plan_info or {}, lanes=lane_info)
 
     if args.pmc_child:  # under rocprofv3 --pmc: a warm-up and two frames of the production kernel
         for i in range(3):
@@ -605,6 +636,10 @@ def main():
     ap.add_argument("--plan", default=None, choices=["cost", "rr"],
                     help="tile order / deal: cost (default: a probe frame's per-wave clocks, heaviest tiles first, "
                          "longest-processing-time deal over ranks) or round-robin in row-major order")
+    ap.add_argument("--lanes", default="auto", choices=["auto", "on", "off"],
+                    help="lane plan (rt_lane_plan: split the waves of the frame's costliest pixels); auto = on for N > 1")
+    ap.add_argument("--lane-units", type=float, default=48000.0,
+                    help="rt_lane_plan parallel_units (MI355X: 48000 measured best for configs 2 and 3 at N = 2-8)")
     ap.add_argument("--tune", type=lambda s: int(s, 0), default=0, help="diagnostic A/B knobs (0 = production)")
     ap.add_argument("--foreign", action="store_true",
                     help="render a GPUScene filled outside this library (the reference's Scene::Upload pattern): "

@@ -66,7 +66,8 @@ class RenderParams(ctypes.Structure):
                 ("shard_index", ctypes.c_int32), ("shard_count", ctypes.c_int32), ("flags", ctypes.c_int32),
                 ("out_shard", ctypes.c_void_p), ("stats", ctypes.c_void_p), ("segment_counter", ctypes.c_void_p),
                 ("tile_list", ctypes.c_void_p), ("tile_count", ctypes.c_int64), ("wave_clock", ctypes.c_void_p),
-                ("tune", ctypes.c_uint32)]
+                ("tune", ctypes.c_uint32), ("lane_slots", ctypes.c_void_p), ("lane_slot_count", ctypes.c_int64),
+                ("lane_cost", ctypes.c_void_p), ("priority_waves", ctypes.c_int64)]
 
 
 assert ctypes.sizeof(GPUScene) == 136 and ctypes.sizeof(GPUMaterial) == 64
@@ -85,6 +86,8 @@ SIGNATURES = {
     "rt_unshard": (_I, [_P, _U64, _I, _I, _I, _P, ctypes.c_int64, _P]),
     "rt_shard_plan_capacity": (ctypes.c_int64, [_I, _I, _I]),
     "rt_shard_plan": (_I, [_I, _I, _I, _P, ctypes.c_int64, _P, _P]),
+    "rt_lane_plan_capacity": (ctypes.c_int64, [ctypes.c_int64]),
+    "rt_lane_plan": (ctypes.c_int64, [_P, ctypes.c_int64, ctypes.c_double, ctypes.c_double, _P, ctypes.c_int64, _P]),
     "rt_init_rng_tiles": (_I, [_P, _I, _I, _P, ctypes.c_int64, _U32, _P]),
     "rt_unshard_tiles": (_I, [_P, _U64, _I, _I, _I, _P, ctypes.c_int64, _P, _P]),
     "rt_comm_unique_id": (_I, [_P]),
@@ -329,18 +332,27 @@ def init_rng_states(rng, width, height, seed, shard_index=0, shard_count=1, stre
 
 def render(scene, surface, last, width, height, spp, bounces, frame_index=0, shard_index=0, shard_count=1,
            out_shard=None, stats=None, segment_counter=None, stream=None, tracer="fast", tile_list=None,
-           wave_clock=None, tune=0):
+           wave_clock=None, tune=0, lane_slots=None, lane_cost=None, priority_waves=0):
     """rt_render: one frame (or one shard of it) on `stream` (default: torch's current stream).
     tile_list: device int32 tensor of tile ids (a row of a sharding.Plan) instead of the
     round-robin deal; wave_clock: device int64 tensor [entries*4] receiving per-wave clocks;
-    tune: diagnostic A/B knobs (0 = production)."""
+    tune: diagnostic A/B knobs (0 = production); lane_slots: device int32 lane map (rt_lane_plan,
+    a multiple of 64 entries); lane_cost: device int32/uint32 [slots] receiving per-pixel clocks."""
     p = RenderParams()
+    if lane_slots is not None:
+        assert lane_slots.dtype == torch.int32 and lane_slots.is_cuda and lane_slots.numel() % 64 == 0
+        p.lane_slots, p.lane_slot_count = lane_slots.data_ptr(), lane_slots.numel()
+        p.priority_waves = int(priority_waves)
+    if lane_cost is not None:
+        assert lane_cost.dtype == torch.int32 and lane_cost.is_cuda
+        p.lane_cost = lane_cost.data_ptr()
     if tile_list is not None:
         assert tile_list.dtype == torch.int32 and tile_list.is_cuda and tile_list.dim() == 1
         p.tile_list, p.tile_count = tile_list.data_ptr(), tile_list.numel()
     if wave_clock is not None:
         n = tile_list.numel() if tile_list is not None else tiles_of(width, height, shard_index, shard_count)
-        assert wave_clock.dtype == torch.int64 and wave_clock.numel() >= 4 * n
+        waves = lane_slots.numel() // 64 if lane_slots is not None else 4 * n
+        assert wave_clock.dtype == torch.int64 and wave_clock.numel() >= waves
         p.wave_clock = wave_clock.data_ptr()
     p.tune = int(tune)
     p.surface = surface.data_ptr() if surface is not None else None
@@ -402,6 +414,20 @@ def shard_plan(width, height, shard_count, tile_cost=None):
     _check(lib().rt_shard_plan(width, height, shard_count, cost_ptr, cap, lists.ctypes.data, counts.ctypes.data),
            "rt_shard_plan")
     return lists, counts
+
+
+def lane_plan(cost, parallel_units=24000.0, slack=1.0):
+    """rt_lane_plan: (int32 numpy lane map, number of leading long waves) from per-slot work
+    (numpy uint32/int32 [slots], a probe frame's lane_cost)."""
+    cost = np.ascontiguousarray(np.asarray(cost).astype(np.uint32))
+    cap = int(lib().rt_lane_plan_capacity(cost.size))
+    out = np.empty(max(cap, 1), dtype=np.int32)
+    nlong = ctypes.c_int64(0)
+    n = int(lib().rt_lane_plan(cost.ctypes.data, cost.size, float(parallel_units), float(slack), out.ctypes.data, cap,
+                               ctypes.byref(nlong)))
+    if n < 0:
+        raise RTError("rt_lane_plan failed: " + lib().rt_last_error().decode(errors="replace"))
+    return out[:n].copy(), int(nlong.value)
 
 
 def init_rng_tiles(rng, width, height, tile_list, seed, stream=None):

@@ -41,7 +41,11 @@ struct RenderArgs {
     int width, height, frame_index, spp, bounces;
     int shard_index, shard_count, tiles_x;
     const int32_t* tile_list;        // tile of list entry k (rt_render_params.tile_list) or null: round-robin
-    unsigned long long* wave_clock;  // per-wave elapsed clock ticks, [list entry][4 sub-tiles], or null
+    unsigned long long* wave_clock;  // per-wave elapsed clock ticks, [list entry][4 sub-tiles] (or [wave] with a lane map), or null
+    const int32_t* lane_slots;       // lane map: wave w lane l renders slot lane_slots[64w + l] (< 0 idle), or null
+    long long slot_count;            // slots of the launch's list (tiles x 256): larger map entries are idle lanes
+    uint32_t* lane_cost;             // per-slot work of a probe frame (timing kernel), or null
+    int priority_waves;              // lane map: waves below this index run at raised priority
     const int* gate;                 // foreign scenes: the kernel runs only if *gate == gate_value
     int gate_value;
     unsigned long long* stats;
@@ -65,6 +69,7 @@ struct Counters {
     unsigned long long ktest = 0, ktri = 0;  // leaf-tree node visits / triangle tests
     unsigned long long cy_small = 0, cy_big = 0, r_coop = 0, r_shared = 0, coop_rays = 0, w_iter = 0;  // timing
     unsigned long long cy_tcl = 0, cy_ttri = 0, cy_tree = 0;  // timing: leaf-tree cluster / triangle rounds, whole walk
+    uint32_t lane_work = 0;  // timing: this lane's own traversal steps (+3 per big leaf), rt_render_params.lane_cost
 };
 
 __device__ __forceinline__ rtm::f3 ld3(const float* p) { return rtm::f3{p[0], p[1], p[2]}; }

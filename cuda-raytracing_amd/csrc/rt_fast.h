@@ -933,9 +933,13 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                 const uint32_t qv = (tune >> 13) & 7u, q = qv ? qv - 1u : 1u;
                 if (TIMING) c.w_small++, c.l_small += inner || leafs;
                 if (!mI || nL * 4u >= nI * (q + 1u)) {
-                    if (leafs) active = small_step<STATS>(nodes4, tris, spairs, stk, R, h, T, c);
+                    if (leafs) {
+                        active = small_step<STATS>(nodes4, tris, spairs, stk, R, h, T, c);
+                        if (TIMING) c.lane_work++;
+                    }
                 } else if (inner) {
                     active = small_step<STATS>(nodes4, tris, spairs, stk, R, h, T, c);
+                    if (TIMING) c.lane_work++;
                 }
                 continue;
             }
@@ -949,7 +953,10 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                 c.w_small++;
                 c.l_small += small;
             }
-            if (small) active = small_step<STATS>(nodes4, tris, spairs, stk, R, h, T, c);
+            if (small) {
+                active = small_step<STATS>(nodes4, tris, spairs, stk, R, h, T, c);
+                if (TIMING) c.lane_work++;
+            }
             continue;
         }
         if (TIMING) {
@@ -959,8 +966,11 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
         }
         const unsigned long long big = __ballot(active);  // every active lane waits at a big leaf
         if (!big) break;
-        if (big_round<STATS, MODE>(tris, pairs, tree, ltris, flat, scratch, tune, big, active, R, h, T, c))
+        if (big_round<STATS, MODE>(tris, pairs, tree, ltris, flat, scratch, tune, big, active, R, h, T, c)) {
+            // a big leaf run alone (cooperative round) costs about as much as 3 small steps
+            if (TIMING) c.lane_work += 3;
             active = pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
+        }
         if (TIMING) {
             const unsigned long long t1 = __builtin_amdgcn_s_memtime();
             c.cy_big += t1 - t0;

@@ -421,7 +421,7 @@ __global__ __launch_bounds__(WAVE) void render_kernel(RenderArgs a) {
     const int y = (tile / a.tiles_x) * TILE + ly;
     Counters c;
     if (tile >= 0 && x < a.width && y < a.height) {  // off-frame lanes stay for the wave reduction
-        const size_t slot = (size_t)k * (TILE * TILE) + tid;
+        const size_t slot = (size_t)(k >= 0 ? k : 0) * (TILE * TILE) + tid;
         const size_t rng_index = a.out_shard ? slot : (size_t)y * a.width + x;
         shade_pixel<Tracer, STACK, STATS>(a, stk, x, y, rng_index, slot, c);
     }
@@ -537,16 +537,21 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
     const float4* tris = reinterpret_cast<const float4*>(a.tris);
     // one 64-lane workgroup per 8x8 sub-tile: tile k = lb / 4, sub-tile lb % 4
     const int lb = xcd_block(a.tune);
-    const int k = lb >> 2;
-    const int tid = ((lb & 3) << 6) | (int)threadIdx.x;
-    const int tile = shard_tile(a, k);
+    int k = lb >> 2, tid = ((lb & 3) << 6) | (int)threadIdx.x;
+    if (a.lane_slots) {  // lane map (rt_lane_plan): any slot on any lane, same pixels bit for bit
+        const int s = a.lane_slots[(size_t)lb * WAVE + threadIdx.x];
+        const bool ok = s >= 0 && (long long)s < a.slot_count;  // a bad map entry renders nothing
+        k = ok ? s >> 8 : -1, tid = s & 255;
+        if (lb < a.priority_waves) __builtin_amdgcn_s_setprio(3);  // the frame's long waves
+    }
+    const int tile = k >= 0 ? shard_tile(a, k) : -1;
     int lx, ly;
     tile_pixel(tid, &lx, &ly);
     const int x = (tile % a.tiles_x) * TILE + lx;
     const int y = (tile / a.tiles_x) * TILE + ly;
     Counters c;
     bool pixel = tile >= 0 && x < a.width && y < a.height;
-    const size_t slot = (size_t)k * (TILE * TILE) + tid;
+    const size_t slot = (size_t)(k >= 0 ? k : 0) * (TILE * TILE) + tid;
     rt_rng_state* rs = a.rng + (a.out_shard ? slot : (size_t)(pixel ? y : 0) * a.width + (pixel ? x : 0));
     rtm::Xorwow rng{0, 0, 0, 0, 0, 0};
     if (pixel) rng = rtm::Xorwow{rs->d, rs->v[0], rs->v[1], rs->v[2], rs->v[3], rs->v[4]};
@@ -603,6 +608,8 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
                 rs->v[2] = rng.v2;
                 rs->v[3] = rng.v3;
                 rs->v[4] = rng.v4;
+                // per-pixel work for rt_lane_plan: traversal steps + 3 per big leaf + 1 per segment
+                if ((MODE & 8) && a.lane_cost) a.lane_cost[slot] = c.lane_work + (uint32_t)c.seg;
             }
         }
         if (!__ballot(path)) break;
@@ -820,51 +827,54 @@ hipError_t launch(const RenderArgs& args, int waves, hipStream_t stream) {
 }
 
 template <int STACK, bool STATS, int MODE>
-hipError_t launch_fast_m(const RenderArgs& args, int tiles, hipStream_t stream) {
+hipError_t launch_fast_m(const RenderArgs& args, int waves, hipStream_t stream) {
     // default: 5 waves per SIMD (96 VGPRs, a few cold spills; 4 % faster than the compiler's 126)
     const uint32_t occ = (args.tune >> 9) & 3u;
     if (!STATS && occ == 0)
-        hipLaunchKernelGGL((render_fast_kernel_w5<STACK, STATS, MODE>), dim3(tiles * 4), dim3(WAVE), 0, stream, args);
+        hipLaunchKernelGGL((render_fast_kernel_w5<STACK, STATS, MODE>), dim3(waves), dim3(WAVE), 0, stream, args);
     else if (!STATS && occ == 2)
-        hipLaunchKernelGGL((render_fast_kernel_w6<STACK, STATS, MODE>), dim3(tiles * 4), dim3(WAVE), 0, stream, args);
+        hipLaunchKernelGGL((render_fast_kernel_w6<STACK, STATS, MODE>), dim3(waves), dim3(WAVE), 0, stream, args);
     else
-        hipLaunchKernelGGL((render_fast_kernel<STACK, STATS, MODE>), dim3(tiles * 4), dim3(WAVE), 0, stream, args);
+        hipLaunchKernelGGL((render_fast_kernel<STACK, STATS, MODE>), dim3(waves), dim3(WAVE), 0, stream, args);
     return hipGetLastError();
 }
 
 template <int STACK, bool STATS>
-hipError_t launch_fast_t(const RenderArgs& args, int tiles, hipStream_t stream) {
+hipError_t launch_fast_t(const RenderArgs& args, int waves, hipStream_t stream) {
 
     // statistics: the reference's work on scalar records (RT_TUNE bit 7: through the leaf trees);
     // RT_TUNE bit 8: a timing frame of the production kernel instead (phase clocks, no counts)
     if (STATS && (args.tune & 256u))
-        return args.tree ? launch_fast_m<STACK, false, 29>(args, tiles, stream)
-               : (args.tune & 4096u) ? launch_fast_m<STACK, false, 9>(args, tiles, stream)
-                                     : launch_fast_m<STACK, false, 25>(args, tiles, stream);
-    if (STATS) return (args.tree && (args.tune & 128u)) ? launch_fast_m<STACK, STATS, 6>(args, tiles, stream)
-                                                        : launch_fast_m<STACK, STATS, 2>(args, tiles, stream);
+        return args.tree ? launch_fast_m<STACK, false, 29>(args, waves, stream)
+               : (args.tune & 4096u) ? launch_fast_m<STACK, false, 9>(args, waves, stream)
+                                     : launch_fast_m<STACK, false, 25>(args, waves, stream);
+    // per-pixel work (rt_render_params.lane_cost): the timing variant of the production kernel
+    if (!STATS && args.lane_cost)
+        return args.tree ? launch_fast_m<STACK, false, 29>(args, waves, stream) : launch_fast_m<STACK, false, 25>(args, waves, stream);
+    if (STATS) return (args.tree && (args.tune & 128u)) ? launch_fast_m<STACK, STATS, 6>(args, waves, stream)
+                                                        : launch_fast_m<STACK, STATS, 2>(args, waves, stream);
     // big leaves: packed pairs in the shared-leaf loop, scalar records in cooperative rounds
     // (MODE 1, measured best), leaf trees compiled in only for scenes that have them (MODE 5);
     // A/B: RT_TUNE bits 4-5 = 2 scalar only, 3 pairs everywhere
     // MODE bit 4: inner-node and small-leaf steps in separate iterations (rt_fast.h trace);
     // RT_TUNE bit 12 turns it off (A/B)
     const bool split = (args.tune & 4096u) == 0;
-    if (args.tree) return split ? launch_fast_m<STACK, STATS, 21>(args, tiles, stream)
-                                : launch_fast_m<STACK, STATS, 5>(args, tiles, stream);
+    if (args.tree) return split ? launch_fast_m<STACK, STATS, 21>(args, waves, stream)
+                                : launch_fast_m<STACK, STATS, 5>(args, waves, stream);
     const uint32_t mode = (args.tune >> 4) & 3u;
-    if (mode == 2) return launch_fast_m<STACK, STATS, 2>(args, tiles, stream);
-    if (mode == 3) return launch_fast_m<STACK, STATS, 0>(args, tiles, stream);
-    return split ? launch_fast_m<STACK, STATS, 17>(args, tiles, stream) : launch_fast_m<STACK, STATS, 1>(args, tiles, stream);
+    if (mode == 2) return launch_fast_m<STACK, STATS, 2>(args, waves, stream);
+    if (mode == 3) return launch_fast_m<STACK, STATS, 0>(args, waves, stream);
+    return split ? launch_fast_m<STACK, STATS, 17>(args, waves, stream) : launch_fast_m<STACK, STATS, 1>(args, waves, stream);
 }
 
-hipError_t launch_fast(const RenderArgs& args, int tiles, int depth, bool stats, hipStream_t s) {
+hipError_t launch_fast(const RenderArgs& args, int waves, int depth, bool stats, hipStream_t s) {
     // 30 entries: 7.5 KB of LDS per wave (+256 B scratch in tree scenes) still fits 5 waves per
     // SIMD, and covers the 4-bunny scene's depth 28 (STACK 40 would leave it at 3 waves per SIMD)
     if (depth >= 0 && depth + 2 <= 30)
-        return stats ? launch_fast_t<30, true>(args, tiles, s) : launch_fast_t<30, false>(args, tiles, s);
+        return stats ? launch_fast_t<30, true>(args, waves, s) : launch_fast_t<30, false>(args, waves, s);
     if (depth >= 0 && depth + 2 <= 40)
-        return stats ? launch_fast_t<40, true>(args, tiles, s) : launch_fast_t<40, false>(args, tiles, s);
-    return stats ? launch_fast_t<64, true>(args, tiles, s) : launch_fast_t<64, false>(args, tiles, s);
+        return stats ? launch_fast_t<40, true>(args, waves, s) : launch_fast_t<40, false>(args, waves, s);
+    return stats ? launch_fast_t<64, true>(args, waves, s) : launch_fast_t<64, false>(args, waves, s);
 }
 
 template <class Tracer>
@@ -1243,6 +1253,13 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     a.wave_clock = (unsigned long long*)p->wave_clock;
     const int tiles = p->tile_list ? (int)p->tile_count : tiles_of_shard(p->width, p->height, p->shard_index, p->shard_count);
     if (tiles == 0) return 0;
+    if (p->lane_slots && (p->lane_slot_count <= 0 || p->lane_slot_count % WAVE != 0 || p->lane_slot_count > (int64_t)1 << 30))
+        return set_error("rt_render: lane_slots needs a positive multiple of 64 entries (< 2^30)");
+    a.lane_slots = p->lane_slots;
+    a.slot_count = (long long)tiles * TILE * TILE;
+    a.lane_cost = p->lane_cost;
+    a.priority_waves = p->lane_slots ? (int)std::min<int64_t>(std::max<int64_t>(p->priority_waves, 0), 1 << 30) : 0;
+    const int waves = p->lane_slots ? (int)(p->lane_slot_count / WAVE) : tiles * 4;  // production tracer's grid
     // Every device buffer must cover what the launch touches: a short buffer would fault the GPU.
     {
         const bool compact = p->out_shard != nullptr;
@@ -1257,9 +1274,12 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
         if (!compact && p->surface_last_frame && bytes_from(p->surface_last_frame) < frame)
             return set_error("rt_render: surface_last_frame too small");
         if (p->tile_list && bytes_from(p->tile_list) < (size_t)tiles * 4) return set_error("rt_render: tile_list too small");
-        if (p->wave_clock && bytes_from(p->wave_clock) < (size_t)tiles * 4 * 8)
+        if (p->wave_clock && bytes_from(p->wave_clock) < (size_t)waves * 8)
             return set_error("rt_render: wave_clock too small");
-        const size_t stats_need = (RT_STAT_COUNT + ((p->tune & 2048u) ? (size_t)tiles * 4 * 8 : 0)) * 8;
+        if (p->lane_slots && bytes_from(p->lane_slots) < (size_t)p->lane_slot_count * 4)
+            return set_error("rt_render: lane_slots too small");
+        if (p->lane_cost && bytes_from(p->lane_cost) < slots * 4) return set_error("rt_render: lane_cost too small");
+        const size_t stats_need = (RT_STAT_COUNT + ((p->tune & 2048u) ? (size_t)waves * 8 : 0)) * 8;
         if (p->stats && bytes_from(p->stats) < stats_need) return set_error("rt_render: stats too small");
     }
     const bool want_ref = (p->flags & RT_RENDER_TRACER_REF) != 0;
@@ -1284,11 +1304,13 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     const bool stats = (p->flags & RT_RENDER_STATS) != 0;
     hipStream_t s = (hipStream_t)stream;
     const bool want_flat = (p->flags & RT_RENDER_TRACER_FLAT) != 0;
+    if ((p->lane_slots || p->lane_cost) && (gate || !a.tris || want_flat))
+        return set_error("rt_render: lane_slots / lane_cost need the production tracer on an rt_scene_upload scene");
     a.scene_fast = scene_fast ? 1 : 0;
     hipError_t e;
     if (gate) {  // foreign scene with a mirror: exactly one of the two runs, by the frame's fingerprint
         a.gate = gate, a.gate_value = 1;
-        e = want_flat ? launch_variant<FlatTracer>(a, tiles * 4, depth, stats, s) : launch_fast(a, tiles, depth, stats, s);
+        e = want_flat ? launch_variant<FlatTracer>(a, tiles * 4, depth, stats, s) : launch_fast(a, waves, depth, stats, s);
         if (e == hipSuccess) {
             RenderArgs r = a;
             r.tris = nullptr, r.gate_value = 0;
@@ -1299,7 +1321,7 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     else if (want_flat)
         e = launch_variant<FlatTracer>(a, tiles * 4, depth, stats, s);
     else
-        e = launch_fast(a, tiles, depth, stats, s);
+        e = launch_fast(a, waves, depth, stats, s);
     return check(e, "render_kernel launch");
 }
 

@@ -75,3 +75,120 @@ extern "C" int rt_shard_plan(int width, int height, int shard_count, const doubl
     }
     return 0;
 }
+
+// ---------------------------------------------------------------------------------------
+// Lane plans (rt_render_params.lane_slots).  A wave takes as long as the union of its lanes'
+// traversal steps, so a 64-pixel wave of expensive pixels (rays trapped between the bunny's base
+// and the floor leaf) runs ~4x longer than its costliest pixel alone: the heaviest 16x16 tile of
+// config 2 renders in 9.6 ms as 4 waves of 64 pixels, 6.8 ms as 16 waves of 16, 3.9 ms as 64
+// waves of 4 and 2.4 ms as 256 one-pixel waves (bit-identical; tools/heavy_probe.py) -- about
+// max x (pixels)^0.34.  Once a frame is split over enough ranks, those waves are each rank's
+// whole frame time.
+//
+// Model: a wave of pixels with probe-frame work c_i (rt_render_params.lane_cost) takes about
+// E = max c x (sum c / max c)^0.34 work units, a lone lane running one unit per unit of time;
+// the whole rank needs about sum c / P units of time when the GPU is full, P = the lanes' worth
+// of work the device does in parallel (MI355X, config 2: 16.4 ms for 634 M units, 2.4 ms for the
+// 3,970-unit pixel alone: P ~ 24,000).  The plan keeps every 8x8 sub-tile wave whose E is within
+// the target B = slack x max(max c, sum c / P) and splits the others (their pixels in decreasing
+// work, first fit into sub-waves of E <= B: pixels of one sub-tile stay together, so their rays
+// stay coherent).  Waves with E >= B / 2 go first, longest first (the tail starts at t = 0), the
+// rest follow in list order (cost-ordered plans put the heaviest tiles first).
+// ---------------------------------------------------------------------------------------
+namespace {
+constexpr double kLaneExp = 0.34;  // wave time ~ max x (sum / max)^0.34 (measured, see above)
+
+double wave_units(double mx, double sum) { return mx > 0 ? mx * std::pow(sum / mx, kLaneExp) : 0.0; }
+}  // namespace
+
+extern "C" int64_t rt_lane_plan_capacity(int64_t slots) {
+    if (slots <= 0 || slots % 64 != 0) return 0;
+    return 4 * slots;  // splitting stops once the plan holds four times the sub-tile waves
+}
+
+extern "C" int64_t rt_lane_plan(const uint32_t* cost, int64_t slots, double parallel_units, double slack,
+                                int32_t* lane_slots, int64_t capacity, int64_t* long_waves) {
+    if (!cost || !lane_slots || slots <= 0 || slots % 64 != 0 || slots > ((int64_t)1 << 30) ||
+        capacity < rt_lane_plan_capacity(slots) || !(slack > 0) || !(parallel_units == parallel_units)) {
+        rt_internal_set_error("rt_lane_plan: bad arguments (slots must be a positive multiple of 64, capacity >= "
+                              "rt_lane_plan_capacity(slots), slack > 0)");
+        return -1;
+    }
+    const int64_t nw = slots / 64, max_waves = capacity / 64;
+    double cmax = 0, csum = 0;
+    for (int64_t s = 0; s < slots; s++) cmax = std::max(cmax, (double)cost[s]), csum += cost[s];
+    const double B = parallel_units > 0 ? slack * std::max(cmax, csum / parallel_units) : 0.0;
+    struct Wave {
+        std::vector<int32_t> lanes;
+        double mx = 0, sum = 0;
+        int64_t order = 0;
+    };
+    // sub-tile waves, split longest first (so a capped plan leaves only the shortest ones whole)
+    std::vector<Wave> tile(nw);
+    std::vector<double> e0(nw);
+    for (int64_t w = 0; w < nw; w++) {
+        tile[w].order = w;
+        for (int l = 0; l < 64; l++) {
+            const int32_t s = (int32_t)(w * 64 + l);
+            tile[w].lanes.push_back(s);
+            tile[w].mx = std::max(tile[w].mx, (double)cost[s]), tile[w].sum += cost[s];
+        }
+        e0[w] = wave_units(tile[w].mx, tile[w].sum);
+    }
+    std::vector<int64_t> by_e(nw);
+    std::iota(by_e.begin(), by_e.end(), 0);
+    std::stable_sort(by_e.begin(), by_e.end(), [&](int64_t a, int64_t b) { return e0[a] > e0[b]; });
+    std::vector<std::vector<Wave>> split(nw);
+    int64_t total = nw;
+    for (int64_t w : by_e) {
+        if (B <= 0 || e0[w] <= B) break;
+        std::vector<int32_t> by = tile[w].lanes;
+        std::stable_sort(by.begin(), by.end(), [&](int32_t a, int32_t b) { return cost[a] > cost[b]; });
+        std::vector<Wave> sub;
+        for (int32_t s : by) {
+            const double c = cost[s];
+            bool placed = false;
+            for (Wave& v : sub)
+                if (v.lanes.size() < 64 && (c == 0 || wave_units(v.mx, v.sum + c) <= B)) {  // v.mx >= c (decreasing)
+                    v.lanes.push_back(s), v.sum += c, placed = true;
+                    break;
+                }
+            if (!placed) {
+                Wave v;
+                v.order = w, v.mx = c, v.sum = c;
+                v.lanes.push_back(s);
+                sub.push_back(std::move(v));
+            }
+        }
+        if (total + (int64_t)sub.size() - 1 > max_waves) break;  // no room: the rest stay whole
+        total += (int64_t)sub.size() - 1;
+        split[w] = std::move(sub);
+    }
+    std::vector<Wave> out;
+    out.reserve(total);
+    for (int64_t w = 0; w < nw; w++) {
+        if (split[w].empty()) out.push_back(std::move(tile[w]));
+        else for (Wave& v : split[w]) out.push_back(std::move(v));
+    }
+    // long waves (E >= B / 2) first, longest first; then the others in list order
+    std::vector<double> e(out.size());
+    for (size_t i = 0; i < out.size(); i++) e[i] = wave_units(out[i].mx, out[i].sum);
+    std::vector<int64_t> idx(out.size());
+    std::iota(idx.begin(), idx.end(), 0);
+    int64_t nlong = 0;
+    for (size_t i = 0; i < out.size(); i++) nlong += (B > 0 && e[i] >= 0.5 * B) ? 1 : 0;
+    std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) {
+        const bool la = B > 0 && e[a] >= 0.5 * B, lb = B > 0 && e[b] >= 0.5 * B;
+        if (la != lb) return la;
+        if (la) return e[a] > e[b];
+        return out[a].order < out[b].order;
+    });
+    int64_t n = 0;
+    for (int64_t i : idx) {
+        const Wave& v = out[i];
+        for (int l = 0; l < 64; l++) lane_slots[n + l] = l < (int)v.lanes.size() ? v.lanes[l] : -1;
+        n += 64;
+    }
+    if (long_waves) *long_waves = nlong;
+    return n;
+}

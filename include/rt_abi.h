@@ -175,6 +175,19 @@ typedef struct rt_render_params {
      * of the production tracer (the cost input of rt_shard_plan). */
     uint64_t* wave_clock;
     uint32_t tune;                 /* diagnostic A/B knobs (tools/); 0 = the production path */
+    /* Optional lane map (production tracer only): wave w, lane l renders slot lane_slots[64w + l]
+     * (slot k*256 + t = thread t of list entry k, as in the layout rule below; < 0 = idle lane)
+     * instead of slot 64w + l.  lane_slot_count (a multiple of 64) sets the number of waves.  Any
+     * permutation renders the same pixels bit for bit; rt_lane_plan builds one that isolates the
+     * costliest pixels (the serial tail of a strong-scaled frame). */
+    const int32_t* lane_slots;
+    int64_t lane_slot_count;
+    /* Optional DEVICE uint32 [slots]: shader-clock ticks from the start of a slot's wave until
+     * its pixel finished (production tracer; the cost input of rt_lane_plan). */
+    uint32_t* lane_cost;
+    /* With a lane map: the first priority_waves waves (rt_lane_plan's long waves) issue at raised
+     * wave priority, so the frame's serial tail does not queue behind the short waves. */
+    int64_t priority_waves;
 } rt_render_params;
 
 /* Layout rule: with out_shard set, RNG state s and output s are compact in list order
@@ -257,6 +270,19 @@ int64_t rt_shard_plan_capacity(int width, int height, int shard_count);
  * below capacity; every rank's list comes out heaviest first.  Deterministic.  0 or error. */
 int rt_shard_plan(int width, int height, int shard_count, const double* tile_cost, int64_t capacity,
                   int32_t* tile_lists, int64_t* counts);
+/* Lane plans (rt_render_params.lane_slots; shard.cpp).  Entries a plan for `slots` slots (a
+ * multiple of 64: 256 per list entry) may use. */
+int64_t rt_lane_plan_capacity(int64_t slots);
+/* Fill HOST lane_slots from HOST per-slot work `cost` (rt_render_params.lane_cost of a probe
+ * frame of the same list, zero for slots without a pixel).  A wave's time is modelled as
+ * max c x (sum c / max c)^0.34 work units; every 8x8 sub-tile wave above the target
+ * slack x max(max c, sum c / parallel_units) is split (first fit, heaviest pixels first) into
+ * sub-waves within it.  Waves of at least half the target go first, longest first; the rest keep
+ * list order.  parallel_units <= 0: the identity map.  parallel_units ~ 24000 on MI355X (shard.cpp).
+ * *long_waves (optional) receives the number of those leading waves (rt_render_params.
+ * priority_waves).  Returns the entries written (a multiple of 64), or -1 on bad arguments. */
+int64_t rt_lane_plan(const uint32_t* cost, int64_t slots, double parallel_units, double slack,
+                     int32_t* lane_slots, int64_t capacity, int64_t* long_waves);
 /* rt_init_rng for an explicit tile list (DEVICE int32): state k*256 + t <- curand_init(seed,
  * pixel id of thread t of tile tile_list[k]). */
 int rt_init_rng_tiles(void* rng_states, int width, int height, const int32_t* tile_list, int64_t tile_count,

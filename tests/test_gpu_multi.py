@@ -103,6 +103,101 @@ def test_single_gpu_tile_order_is_free(rt):
     assert np.array_equal(rng_got, rng_full)
 
 
+def lane_costs(rt, s, w, h, spp, bounces, mine, n, r):
+    """Per-pixel work of one probe frame of a shard (rt_render_params.lane_cost)."""
+    rng = rt.alloc_rng(mine.numel() * 256)
+    rt.init_rng_tiles(rng, w, h, mine, T.SEED)
+    s.upload(rng.data_ptr())
+    out = torch.zeros((mine.numel() * 256, 4), dtype=torch.float32, device="cuda")
+    cost = torch.zeros(mine.numel() * 256, dtype=torch.int32, device="cuda")
+    rt.render(s, None, None, w, h, spp, bounces, 0, r, n, out_shard=out, tile_list=mine, lane_cost=cost)
+    torch.cuda.synchronize()
+    return cost.cpu().numpy()
+
+
+@pytest.mark.parametrize("n,mode", [(1, "plan"), (4, "plan"), (2, "random")])
+def test_lane_map_shards_equal_full(rt, n, mode):
+    """Probe per-pixel work -> rt_lane_plan (aggressive: every sub-tile wave above the costliest
+    pixel's modelled time is split) or a random permutation with idle lanes -> the sharded frames
+    rendered through the lane map == the unsharded frames, bit for bit (pixels, RNG progression
+    over two progressive frames)."""
+    w, h, spp, bounces, frames = 120, 72, 2, 6, 2
+    full, _ = full_frames(rt, w, h, spp, bounces, frames)
+    s = scene(rt, w, h)
+    cost = probe_costs(rt, s, w, h, spp, bounces, n)
+    lists, counts = rt.shard_plan(w, h, n, cost)
+    cap = lists.shape[1]
+    shards = torch.zeros((2, n, cap * 256, 4), dtype=torch.float32, device="cuda")
+    gen = np.random.default_rng(n)
+    for r in range(n):
+        mine = torch.from_numpy(lists[r, : counts[r]]).cuda()
+        c = lane_costs(rt, s, w, h, spp, bounces, mine, n, r)
+        xs, ys = rt.sharding.slot_pixels(w, h, r, n, int(counts[r]), lists[r, : counts[r]])
+        inside = (xs >= 0) & (xs < w) & (ys >= 0) & (ys < h)
+        assert (c[inside] > 0).all() and (c[~inside] == 0).all(), "work is reported for exactly the frame's pixels"
+        if mode == "plan":
+            m, nlong = rt.lane_plan(c, 1e12, 1.0)
+            assert m.size > c.size, "the heavy sub-tile waves were split"
+        else:
+            m = np.full(c.size * 2, -1, dtype=np.int32)
+            m[gen.choice(m.size, c.size, replace=False)] = gen.permutation(c.size).astype(np.int32)
+            nlong = 3
+        assert np.array_equal(np.sort(m[m >= 0]), np.arange(c.size))
+        lm = torch.from_numpy(m).cuda()
+        rng = rt.alloc_rng(cap * 256)
+        rt.init_rng_tiles(rng, w, h, mine, T.SEED)
+        s.upload(rng.data_ptr())
+        for f in range(frames):
+            rt.render(s, None, shards[(f + 1) & 1, r], w, h, spp, bounces, f, r, n, out_shard=shards[f & 1, r],
+                      tile_list=mine, lane_slots=lm, priority_waves=nlong)
+        torch.cuda.synchronize()
+    out = rt.alloc_surface(w, h)
+    rt.unshard_tiles(out, w, h, shards[(frames - 1) & 1], torch.from_numpy(lists).cuda())
+    torch.cuda.synchronize()
+    got = rt.surface_view(out, w).cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), full.view(np.uint32)), f"n={n} {mode}"
+
+
+def test_lane_map_full_frame_layout(rt):
+    """N = 1, reference layout (RNG y*W + x, pitched surface) through a lane map == no map."""
+    w, h, spp, bounces = 200, 120, 2, 6
+    full, rng_full = full_frames(rt, w, h, spp, bounces, 2)
+    s = scene(rt, w, h)
+    tiles = rt.sharding.tiles_total(w, h)
+    mine = torch.arange(tiles, dtype=torch.int32, device="cuda")
+    c = lane_costs(rt, s, w, h, spp, bounces, mine, 1, 0)
+    m, nlong = rt.lane_plan(c, 1e12, 1.0)
+    lm = torch.from_numpy(m).cuda()
+    rng = rt.alloc_rng(w * h)
+    rt.init_rng_states(rng, w, h, T.SEED)
+    s.upload(rng.data_ptr())
+    bufs = [rt.alloc_surface(w, h), rt.alloc_surface(w, h)]
+    for f in range(2):
+        rt.render(s, bufs[f & 1], bufs[(f + 1) & 1], w, h, spp, bounces, f, tile_list=mine, lane_slots=lm,
+                  priority_waves=nlong)
+    torch.cuda.synchronize()
+    got = rt.surface_view(bufs[1], w).cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), full.view(np.uint32))
+    assert np.array_equal(rng.cpu().numpy(), rng_full)
+
+
+def test_lane_map_misuse_is_refused(rt):
+    w, h = 64, 64
+    s = scene(rt, w, h)
+    rng = rt.alloc_rng(w * h)
+    s.upload(rng.data_ptr())
+    a, b = rt.alloc_surface(w, h), rt.alloc_surface(w, h)
+    with pytest.raises(rt.RTError, match="lane"):
+        rt.render(s, a, b, w, h, 1, 1, tracer="ref", lane_cost=torch.zeros(w * h, dtype=torch.int32, device="cuda"))
+    p = rt.RenderParams()
+    p.surface, p.width, p.height, p.pitch, p.spp, p.bounces, p.shard_count = a.data_ptr(), w, h, w * 16, 1, 1, 1
+    lm = torch.zeros(100, dtype=torch.int32, device="cuda")
+    p.lane_slots, p.lane_slot_count = lm.data_ptr(), 100  # not a multiple of 64
+    import ctypes
+    assert rt.lib().rt_render(ctypes.byref(p), ctypes.cast(s.gpu, ctypes.c_void_p), None) != 0
+    torch.cuda.synchronize()
+
+
 def test_rccl_gather_one_rank(rt):
     """rt_gather_shards through the C-ABI (RCCL) with a one-rank communicator: the root's own
     shard lands at its stride offset (the other ranks' path is the same send/recv group)."""
@@ -132,6 +227,7 @@ def test_bench_two_ranks_without_launcher(tmp_path):
     res = json.loads(line)
     assert res["n_gpus"] == 2 and res["check_equal"] is True, res
     assert res["plan"]["kind"].startswith("cost") and sum(res["plan"]["tiles_per_rank"]) == 256
+    assert res["plan"]["lanes"]["waves"] >= 4 * 128, "N > 1 renders through a lane plan by default"
     assert len(res["rank_kernel_ms"]) == 2
 
 

@@ -37,17 +37,52 @@ def probe(rt, scene, W, H, SPP, BOUNCES):
     return cost
 
 
-def time_shard(rt, scene, W, H, SPP, BOUNCES, tiles, r, n, reps):
+def lane_map(rt, scene, W, H, SPP, BOUNCES, mine, rng, lane):
+    """rt_lane_plan of this shard from one probe frame's per-pixel work (lane = (ratio, budget))."""
+    rt.init_rng_tiles(rng, W, H, mine, bench.SEED)
+    out = torch.zeros((mine.numel() * 256, 4), dtype=torch.float32, device="cuda")
+    cost = torch.zeros(mine.numel() * 256, dtype=torch.int32, device="cuda")
+    rt.render(scene, None, None, W, H, SPP, BOUNCES, 0, 0, 1, out_shard=out, tile_list=mine, lane_cost=cost)
+    torch.cuda.synchronize()
+    c = cost.cpu().numpy()
+    if os.environ.get("LANE_SAVE"):  # per-slot probe costs for offline plan work
+        os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+        np.save(os.path.join(ROOT, "gpurun_out", f"lanecost_{os.environ['LANE_SAVE']}_{mine.numel()}_{int(mine[0])}.npy"), c)
+    m, nlong = rt.lane_plan(c, lane[0], lane[1])
+    nlong = nlong if len(lane) < 3 or lane[2] else 0  # lane[2] == 0: no wave priority
+    rt.init_rng_tiles(rng, W, H, mine, bench.SEED)
+    lm = torch.from_numpy(m).cuda()
+    if os.environ.get("LANE_DIAG"):  # which waves are the long ones under this plan
+        clk = torch.zeros(m.size // 64, dtype=torch.int64, device="cuda")
+        rt.render(scene, None, None, W, H, SPP, BOUNCES, 0, 0, 1, out_shard=out, tile_list=mine, lane_slots=lm,
+                  wave_clock=clk, priority_waves=nlong)
+        torch.cuda.synchronize()
+        rt.init_rng_tiles(rng, W, H, mine, bench.SEED)
+        wc = clk.cpu().numpy()
+        mw = m.reshape(-1, 64)
+        nh = int(np.argmax((mw >= 0).sum(1) == 64)) if ((mw >= 0).sum(1) == 64).any() else len(mw)
+        top = np.argsort(-wc)[:5]
+        print(json.dumps({"slots": int(c.size), "cmax": int(c.max()), "csum": int(c.sum()), "R": round(float(c.sum()) / c.max(), 1),
+                          "p99": float(np.percentile(c[c > 0], 99)), "waves": int(len(mw)), "long": nlong, "first_full_wave": nh,
+                          "top_waves": [[int(i), round(float(wc[i]) / 2.4e6, 2), int((mw[i] >= 0).sum()),
+                                         int(c[mw[i][mw[i] >= 0]].max()), int(c[mw[i][mw[i] >= 0]].sum())] for i in top]}),
+              flush=True)
+    return lm, nlong
+
+
+def time_shard(rt, scene, W, H, SPP, BOUNCES, tiles, r, n, reps, lane=None):
     mine = torch.from_numpy(tiles).cuda()
     rng = rt.alloc_rng(len(tiles) * 256)
     rt.init_rng_tiles(rng, W, H, mine, bench.SEED)
     scene.upload(rng.data_ptr())
+    lm, nlong = lane_map(rt, scene, W, H, SPP, BOUNCES, mine, rng, lane) if lane else (None, 0)
     bufs = [torch.zeros((len(tiles) * 256, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
     ms = []
     for i in range(reps + 1):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        rt.render(scene, None, bufs[(i + 1) & 1], W, H, SPP, BOUNCES, i, r, n, out_shard=bufs[i & 1], tile_list=mine)
+        rt.render(scene, None, bufs[(i + 1) & 1], W, H, SPP, BOUNCES, i, r, n, out_shard=bufs[i & 1], tile_list=mine,
+                  lane_slots=lm, priority_waves=nlong)
         e1.record()
         torch.cuda.synchronize()
         if i:
@@ -62,13 +97,16 @@ def main():
     ap.add_argument("--plans", default="rr,cost")
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--weak", action="store_true", help="the frame grows with N as in bench.py --scaling weak")
+    ap.add_argument("--lanes", default="", help="lane plans to try, 'ratio:budget;...' (rt_lane_plan)")
     args = ap.parse_args()
     rt = G.load_package()
     scene_name, W0, H0, SPP, BOUNCES, _ = bench.CONFIGS[args.config]
     torch.cuda.set_device(0)
     res = {"config": args.config, "weak": args.weak, "plans": {}}
     costs = {}
-    for plan in args.plans.split(","):
+    lanes = [None] + [tuple(map(float, x.split(":"))) for x in args.lanes.split(";") if x]
+    plans = [(p, l) for p in args.plans.split(",") for l in lanes]
+    for plan, lane in plans:
         per_n = {}
         for n in map(int, args.ns.split(",")):
             W, H = bench.weak_size(W0, H0, n) if args.weak else (W0, H0)
@@ -81,13 +119,13 @@ def main():
                 lists, counts = rt.shard_plan(W, H, n, costs[(W, H)])
             else:
                 lists, counts = rt.shard_plan(W, H, n)
-            shard_ms = [time_shard(rt, scene, W, H, SPP, BOUNCES, lists[r, : counts[r]], r, n, args.reps)
+            shard_ms = [time_shard(rt, scene, W, H, SPP, BOUNCES, lists[r, : counts[r]], r, n, args.reps, lane)
                         for r in range(n)]
             per_n[n] = shard_ms
-            print(json.dumps({"plan": plan, "n": n, "max_ms": round(max(shard_ms), 3),
+            print(json.dumps({"plan": plan, "lane": lane, "n": n, "max_ms": round(max(shard_ms), 3),
                               "shard_ms": [round(x, 3) for x in shard_ms]}), flush=True)
         t1 = max(per_n[min(per_n)])
-        res["plans"][plan] = {"max_shard_ms": {str(n): round(max(v), 3) for n, v in per_n.items()},
+        res["plans"][plan + ("" if lane is None else f" lane{lane}")] = {"max_shard_ms": {str(n): round(max(v), 3) for n, v in per_n.items()},
                               "shard_ms": {str(n): [round(x, 3) for x in v] for n, v in per_n.items()},
                               "compute_speedup": {str(n): round((n if args.weak else 1) * t1 / max(v), 2)
                                                   for n, v in per_n.items()}}
