@@ -198,7 +198,8 @@ def pmc_pass(args, out_dir, timeout_s=150):
         d = os.path.join(out_dir, f"pass{i}")
         cmd = [rocprof, "--kernel-trace", "--pmc", *cs, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
                sys.executable, os.path.abspath(__file__), "--pmc-child", "--config", args.config,
-               "--plan", args.plan, "--tune", str(args.tune)]
+               "--plan", args.plan, "--tune", str(args.tune), "--refill", str(args.refill),
+               "--lanes", args.lanes, "--lane-units", str(args.lane_units)]
         try:
             r = subprocess.run(cmd, cwd=tempfile.gettempdir(), capture_output=True, text=True, timeout=timeout_s,
                                env=dict(os.environ, TMPDIR=tempfile.gettempdir()))
@@ -406,10 +407,13 @@ def run(args):
     def render(i, cur, prev, **kw):
         if sharded:
             rt.render(scene, None, prev, W, H, SPP, BOUNCES, i, rank, world, out_shard=cur, tile_list=tile_list,
-                      tune=args.tune, lane_slots=lane_slots, **kw)
+                      tune=args.tune, lane_slots=lane_slots, **refill(kw))
         else:
             rt.render(target, cur, prev, W, H, SPP, BOUNCES, i, tile_list=tile_list, tune=args.tune,
-                      lane_slots=lane_slots, **kw)
+                      lane_slots=lane_slots, **refill(kw))
+
+    def refill(kw):  # the probe (lane_cost) runs without refill
+        return kw if "lane_cost" in kw or args.foreign else dict(kw, refill_lanes=args.refill)
 
     # lane plan (rt_lane_plan): split the waves whose pixels form the frame's serial tail
     lanes_on = args.lanes == "on" or (args.lanes == "auto" and sharded)
@@ -636,6 +640,8 @@ def main():
     ap.add_argument("--plan", default=None, choices=["cost", "rr"],
                     help="tile order / deal: cost (default: a probe frame's per-wave clocks, heaviest tiles first, "
                          "longest-processing-time deal over ranks) or round-robin in row-major order")
+    ap.add_argument("--refill", type=int, default=0,
+                    help="rt_render refill_lanes: a wave refills this many idle lanes from the frame's queue (0 = off)")
     ap.add_argument("--lanes", default="auto", choices=["auto", "on", "off"],
                     help="lane plan (rt_lane_plan: split the waves of the frame's costliest pixels); auto = on for N > 1")
     ap.add_argument("--lane-units", type=float, default=48000.0,

@@ -44,6 +44,9 @@ struct RenderArgs {
     unsigned long long* wave_clock;  // per-wave elapsed clock ticks, [list entry][4 sub-tiles] (or [wave] with a lane map), or null
     const int32_t* lane_slots;       // lane map: wave w lane l renders slot lane_slots[64w + l] (< 0 idle), or null
     long long slot_count;            // slots of the launch's list (tiles x 256): larger map entries are idle lanes
+    long long entry_count;           // entries of the lane order (lane map length, or slot_count)
+    unsigned long long* queue_head;  // refill: entries taken from the queue so far (zeroed per launch), or null
+    int refill_lanes;                // refill: idle lanes that trigger a refill
     uint32_t* lane_cost;             // per-slot work of a probe frame (timing kernel), or null
     int priority_waves;              // lane map: waves below this index run at raised priority
     const int* gate;                 // foreign scenes: the kernel runs only if *gate == gate_value

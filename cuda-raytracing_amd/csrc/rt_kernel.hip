@@ -535,26 +535,41 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
     if (a.gate && *a.gate != a.gate_value) return;  // foreign scenes: the other tracer renders this frame
     const float4* nodes4 = reinterpret_cast<const float4*>(a.nodes);
     const float4* tris = reinterpret_cast<const float4*>(a.tris);
+    // this lane's pixel: slot k*256 + tid of the launch's list (k < 0: none)
+    int x = 0, y = 0;
+    bool pixel = false;
+    size_t slot = 0;
+    rt_rng_state* rs = a.rng;
+    rtm::Xorwow rng{0, 0, 0, 0, 0, 0};
+    auto bind = [&](int k, int tid) {
+        const int tile = k >= 0 ? shard_tile(a, k) : -1;
+        int lx, ly;
+        tile_pixel(tid, &lx, &ly);
+        x = (tile % a.tiles_x) * TILE + lx;
+        y = (tile / a.tiles_x) * TILE + ly;
+        pixel = tile >= 0 && x < a.width && y < a.height;
+        slot = (size_t)(k >= 0 ? k : 0) * (TILE * TILE) + tid;
+        rs = a.rng + (a.out_shard ? slot : (size_t)(pixel ? y : 0) * a.width + (pixel ? x : 0));
+        if (pixel) rng = rtm::Xorwow{rs->d, rs->v[0], rs->v[1], rs->v[2], rs->v[3], rs->v[4]};
+    };
+    // entry i of the launch's lane order: the lane map, or slot i (wave i / 64 = 8x8 sub-tile)
+    auto bind_entry = [&](long long i) {
+        const long long s = a.lane_slots ? (long long)a.lane_slots[i] : i;
+        const bool ok = s >= 0 && s < a.slot_count;  // a bad map entry renders nothing
+        bind(ok ? (int)(s >> 8) : -1, (int)(s & 255));
+    };
     // one 64-lane workgroup per 8x8 sub-tile: tile k = lb / 4, sub-tile lb % 4
     const int lb = xcd_block(a.tune);
-    int k = lb >> 2, tid = ((lb & 3) << 6) | (int)threadIdx.x;
-    if (a.lane_slots) {  // lane map (rt_lane_plan): any slot on any lane, same pixels bit for bit
-        const int s = a.lane_slots[(size_t)lb * WAVE + threadIdx.x];
-        const bool ok = s >= 0 && (long long)s < a.slot_count;  // a bad map entry renders nothing
-        k = ok ? s >> 8 : -1, tid = s & 255;
-        if (lb < a.priority_waves) __builtin_amdgcn_s_setprio(3);  // the frame's long waves
-    }
-    const int tile = k >= 0 ? shard_tile(a, k) : -1;
-    int lx, ly;
-    tile_pixel(tid, &lx, &ly);
-    const int x = (tile % a.tiles_x) * TILE + lx;
-    const int y = (tile / a.tiles_x) * TILE + ly;
+    bind_entry((long long)lb * WAVE + threadIdx.x);
+    if (a.lane_slots && lb < a.priority_waves) __builtin_amdgcn_s_setprio(3);  // the frame's long waves
+    // Refill (rt_render_params.refill_lanes): the grid holds only as many waves as fit the GPU at
+    // once; entries [grid x 64, entries) form a queue, and a wave whose idle lanes reach
+    // refill_lanes takes that many entries with one atomic (ballot + mbcnt rank the idle lanes), so
+    // lanes stay busy until the queue drains instead of idling once their own pixel is done.
+    // Waves that start less than half full (split waves of a lane plan) are not refilled.
+    bool drained = a.queue_head == nullptr || __popcll(__ballot(pixel)) < 32;
+    const long long qbase = (long long)gridDim.x * WAVE;
     Counters c;
-    bool pixel = tile >= 0 && x < a.width && y < a.height;
-    const size_t slot = (size_t)(k >= 0 ? k : 0) * (TILE * TILE) + tid;
-    rt_rng_state* rs = a.rng + (a.out_shard ? slot : (size_t)(pixel ? y : 0) * a.width + (pixel ? x : 0));
-    rtm::Xorwow rng{0, 0, 0, 0, 0, 0};
-    if (pixel) rng = rtm::Xorwow{rs->d, rs->v[0], rs->v[1], rs->v[2], rs->v[3], rs->v[4]};
     const rtm::f3 cam_o = ld3(a.cam.origin), cam_h = ld3(a.cam.horizontal), cam_v = ld3(a.cam.vertical),
                   cam_ll = ld3(a.cam.lower_left_corner);
     float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f, acc_a = 0.0f;
@@ -565,6 +580,28 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
     const unsigned long long t_start = ((MODE & 8) || a.wave_clock) ? __builtin_amdgcn_s_memtime() : 0;
 
     for (;;) {
+        if (!drained) {
+            const unsigned long long idle = __ballot(!pixel && !path);
+            const uint32_t ni = (uint32_t)__popcll(idle);
+            if (ni && (ni >= (uint32_t)a.refill_lanes || !__ballot(path))) {
+                const int lead = __ffsll((long long)idle) - 1;
+                unsigned long long base = 0;
+                if ((int)threadIdx.x == lead) base = atomicAdd(a.queue_head, (unsigned long long)ni);
+                base = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(base >> 32), lead) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)base, lead);
+                const long long qn = a.entry_count - qbase;
+                if (!pixel && !path) {
+                    const unsigned long long i =
+                        base + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                    if ((long long)i < qn) {
+                        bind_entry(qbase + (long long)i);
+                        acc_r = acc_g = acc_b = acc_a = 0.0f;
+                        sample = 0;
+                    }
+                }
+                if ((long long)(base + ni) >= qn) drained = true;
+            }
+        }
         if (pixel && !path) {
             if (sample < a.spp) {
                 // main_raytracing.cu:190: uv = (pixel + vec2(rng(), rng())) / vec2(W, H), u first
@@ -612,7 +649,10 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
                 if ((MODE & 8) && a.lane_cost) a.lane_cost[slot] = c.lane_work + (uint32_t)c.seg;
             }
         }
-        if (!__ballot(path)) break;
+        if (!__ballot(path)) {
+            if (drained) break;
+            continue;  // every lane idle: refill at the top
+        }
         if (MODE & 8) c.w_iter++;
         if (STATS) {
             c.w_seg += (threadIdx.x & 63) == 0;
@@ -826,17 +866,58 @@ hipError_t launch(const RenderArgs& args, int waves, hipStream_t stream) {
     return hipGetLastError();
 }
 
+// Waves of `kernel` the device holds at once (refill launches size their grid to it).
+template <class K>
+int resident_waves(K kernel) {
+    static std::mutex mu;
+    static std::map<std::pair<int, const void*>, int> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    std::lock_guard<std::mutex> lock(mu);
+    const auto key = std::make_pair(dev, (const void*)kernel);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    // waves per SIMD from the kernel's registers and LDS (the occupancy query over-counts here)
+    hipFuncAttributes fa;
+    int cus = 0;
+    if (hipFuncGetAttributes(&fa, (const void*)kernel) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    const int vgpr_waves = fa.numRegs > 0 ? std::min(8, 512 / ((fa.numRegs + 7) / 8 * 8)) : 8;
+    const int lds_waves = fa.sharedSizeBytes > 0 ? (int)(160 * 1024 / fa.sharedSizeBytes) / 4 : 8;
+    return cache[key] = std::max(1, std::min(vgpr_waves, lds_waves)) * 4 * std::max(cus, 1);
+}
+
+template <class K>
+hipError_t launch_grid(K kernel, const RenderArgs& args, int waves, hipStream_t stream) {
+    int grid = waves;
+    if (args.queue_head) {  // refill: one grid of resident waves, the rest through the queue
+        const int res = resident_waves(kernel);
+        if (res > 0) grid = std::min(waves, res);
+    }
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(WAVE), 0, stream, args);
+    return hipGetLastError();
+}
+
 template <int STACK, bool STATS, int MODE>
 hipError_t launch_fast_m(const RenderArgs& args, int waves, hipStream_t stream) {
     // default: 5 waves per SIMD (96 VGPRs, a few cold spills; 4 % faster than the compiler's 126)
     const uint32_t occ = (args.tune >> 9) & 3u;
-    if (!STATS && occ == 0)
-        hipLaunchKernelGGL((render_fast_kernel_w5<STACK, STATS, MODE>), dim3(waves), dim3(WAVE), 0, stream, args);
-    else if (!STATS && occ == 2)
-        hipLaunchKernelGGL((render_fast_kernel_w6<STACK, STATS, MODE>), dim3(waves), dim3(WAVE), 0, stream, args);
-    else
-        hipLaunchKernelGGL((render_fast_kernel<STACK, STATS, MODE>), dim3(waves), dim3(WAVE), 0, stream, args);
-    return hipGetLastError();
+    if (!STATS && occ == 0) return launch_grid(render_fast_kernel_w5<STACK, STATS, MODE>, args, waves, stream);
+    if (!STATS && occ == 2) return launch_grid(render_fast_kernel_w6<STACK, STATS, MODE>, args, waves, stream);
+    return launch_grid(render_fast_kernel<STACK, STATS, MODE>, args, waves, stream);
+}
+
+// Per-(device, stream) queue counter of refill launches, zeroed on the stream before each launch.
+unsigned long long* queue_counter(hipStream_t s) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, unsigned long long*> counters;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lock(mu);
+    auto& c = counters[std::make_pair(dev, s)];
+    if (!c && hipMalloc(&c, sizeof(unsigned long long)) != hipSuccess) c = nullptr;
+    return c;
 }
 
 template <int STACK, bool STATS>
@@ -1260,6 +1341,9 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     a.lane_cost = p->lane_cost;
     a.priority_waves = p->lane_slots ? (int)std::min<int64_t>(std::max<int64_t>(p->priority_waves, 0), 1 << 30) : 0;
     const int waves = p->lane_slots ? (int)(p->lane_slot_count / WAVE) : tiles * 4;  // production tracer's grid
+    a.entry_count = (long long)waves * WAVE;
+    if (p->refill_lanes < 0 || p->refill_lanes > 64) return set_error("rt_render: refill_lanes must be in [0, 64]");
+    a.refill_lanes = p->refill_lanes;
     // Every device buffer must cover what the launch touches: a short buffer would fault the GPU.
     {
         const bool compact = p->out_shard != nullptr;
@@ -1304,8 +1388,14 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     const bool stats = (p->flags & RT_RENDER_STATS) != 0;
     hipStream_t s = (hipStream_t)stream;
     const bool want_flat = (p->flags & RT_RENDER_TRACER_FLAT) != 0;
-    if ((p->lane_slots || p->lane_cost) && (gate || !a.tris || want_flat))
-        return set_error("rt_render: lane_slots / lane_cost need the production tracer on an rt_scene_upload scene");
+    if ((p->lane_slots || p->lane_cost || p->refill_lanes) && (gate || !a.tris || want_flat))
+        return set_error("rt_render: lane_slots / lane_cost / refill_lanes need the production tracer on an rt_scene_upload scene");
+    if (p->lane_cost && p->refill_lanes) return set_error("rt_render: lane_cost probes run without refill");
+    if (p->refill_lanes) {  // the queue counter, zeroed on the launch stream
+        a.queue_head = queue_counter(s);
+        if (!a.queue_head) return set_error("rt_render: cannot allocate the refill queue counter");
+        if (check(hipMemsetAsync(a.queue_head, 0, sizeof(unsigned long long), s), "hipMemsetAsync") != 0) return 1;
+    }
     a.scene_fast = scene_fast ? 1 : 0;
     hipError_t e;
     if (gate) {  // foreign scene with a mirror: exactly one of the two runs, by the frame's fingerprint

@@ -188,6 +188,11 @@ typedef struct rt_render_params {
     /* With a lane map: the first priority_waves waves (rt_lane_plan's long waves) issue at raised
      * wave priority, so the frame's serial tail does not queue behind the short waves. */
     int64_t priority_waves;
+    /* Refill (production tracer): 0 = off.  n in [1, 64]: the launch holds only as many waves as
+     * the GPU runs at once; the rest of the lane order (the lane map, or the sub-tile waves) is a
+     * queue, and a wave takes the next n entries as soon as n of its lanes have finished their
+     * pixels (waves that start less than half full keep their lanes to themselves). */
+    int32_t refill_lanes;
 } rt_render_params;
 
 /* Layout rule: with out_shard set, RNG state s and output s are compact in list order

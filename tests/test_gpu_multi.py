@@ -181,6 +181,37 @@ def test_lane_map_full_frame_layout(rt):
     assert np.array_equal(rng.cpu().numpy(), rng_full)
 
 
+@pytest.mark.parametrize("refill,mapped", [(16, False), (1, True), (64, False)])
+def test_refill_equals_full(rt, refill, mapped):
+    """rt_render refill_lanes: a grid of resident waves pulls the rest of the lane order from a
+    queue (ballot + mbcnt over the idle lanes, one atomic per refill) -- any lane may render any
+    pixel at any time, so the frames and the RNG progression equal the plain render bit for bit.
+    The frame is large enough that the queue is long (8160 sub-tile waves for ~5000 resident)."""
+    w, h, spp, bounces = 1920, 1080, 1, 3
+    full, rng_full = full_frames(rt, w, h, spp, bounces, 2)
+    s = scene(rt, w, h)
+    tiles = rt.sharding.tiles_total(w, h)
+    mine = torch.arange(tiles, dtype=torch.int32, device="cuda")
+    lm = None
+    if mapped:
+        m = np.arange(tiles * 256, dtype=np.int32).reshape(-1, 64)
+        m[::7, ::3] = -1  # holes in the queue are skipped
+        rest = np.sort(np.arange(tiles * 256).reshape(-1, 64)[::7, ::3].ravel()).astype(np.int32)
+        m = np.concatenate([m.ravel(), rest, np.full((-rest.size) % 64, -1, np.int32)])
+        lm = torch.from_numpy(m).cuda()
+    rng = rt.alloc_rng(w * h)
+    rt.init_rng_states(rng, w, h, T.SEED)
+    s.upload(rng.data_ptr())
+    bufs = [rt.alloc_surface(w, h), rt.alloc_surface(w, h)]
+    for f in range(2):
+        rt.render(s, bufs[f & 1], bufs[(f + 1) & 1], w, h, spp, bounces, f, tile_list=mine, lane_slots=lm,
+                  refill_lanes=refill)
+    torch.cuda.synchronize()
+    got = rt.surface_view(bufs[1], w).cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), full.view(np.uint32))
+    assert np.array_equal(rng.cpu().numpy(), rng_full)
+
+
 def test_lane_map_misuse_is_refused(rt):
     w, h = 64, 64
     s = scene(rt, w, h)
@@ -195,6 +226,10 @@ def test_lane_map_misuse_is_refused(rt):
     p.lane_slots, p.lane_slot_count = lm.data_ptr(), 100  # not a multiple of 64
     import ctypes
     assert rt.lib().rt_render(ctypes.byref(p), ctypes.cast(s.gpu, ctypes.c_void_p), None) != 0
+    with pytest.raises(rt.RTError, match="refill"):
+        rt.render(s, a, b, w, h, 1, 1, refill_lanes=65)
+    with pytest.raises(rt.RTError, match="without refill"):
+        rt.render(s, a, b, w, h, 1, 1, refill_lanes=8, lane_cost=torch.zeros(w * h, dtype=torch.int32, device="cuda"))
     torch.cuda.synchronize()
 
 
