@@ -8,7 +8,9 @@
 // C-ABI's multi-GPU path (one host thread, N devices): rt_shard_plan deals the 16x16 tiles,
 // each device renders its compact shard (spp 5, 6 bounces as raytracing_process), and
 // rt_gather_shards (RCCL, communicators from rt_comm_init_all) brings the shards to device 0,
-// where rt_unshard_tiles writes the pitched surface.
+// where rt_unshard_tiles writes the pitched surface.  Before the first frame every device runs
+// one probe frame of per-pixel work (rt_render_params.lane_cost, on a copy of its RNG states)
+// and renders through the lane map rt_lane_plan builds from it (bench.py's N > 1 default).
 //
 //   g++ -std=c++17 -Iinclude tests/cpp/host_driver.cpp -Lcuda-raytracing_amd -lrt_hip -o host_driver
 //   ./host_driver out.bin W H frames assets_dir [split]
@@ -68,8 +70,8 @@ static int run_single(const char* path, int w, int h, int frames, const char* as
 
 struct Rank {
     rt_scene* scene = nullptr;
-    void *rng = nullptr, *shard[2] = {nullptr, nullptr}, *tiles = nullptr;
-    int64_t count = 0;
+    void *rng = nullptr, *shard[2] = {nullptr, nullptr}, *tiles = nullptr, *lane_map = nullptr;
+    int64_t count = 0, lanes = 0;
 };
 
 static int run_split(const char* path, int w, int h, int frames, const char* assets) {
@@ -106,6 +108,34 @@ static int run_split(const char* path, int w, int h, int frames, const char* ass
             CHECK(rt_malloc(&r.shard[b], shard_bytes));
             CHECK(rt_memset(r.shard[b], 0, shard_bytes));
         }
+        // lane plan: probe frame of per-pixel work on a copy of the states, then rt_lane_plan
+        const int64_t slots = r.count * 256;
+        void *rng_copy = nullptr, *cost_dev = nullptr;
+        CHECK(rt_malloc(&rng_copy, (size_t)slots * 48));
+        CHECK(rt_memcpy_d2d(rng_copy, r.rng, (size_t)slots * 48));
+        CHECK(rt_malloc(&cost_dev, (size_t)slots * 4));
+        CHECK(rt_memset(cost_dev, 0, (size_t)slots * 4));
+        rt_render_params p;
+        std::memset(&p, 0, sizeof(p));
+        p.width = w, p.height = h, p.spp = 5, p.bounces = 6;
+        p.shard_index = d, p.shard_count = n;
+        p.out_shard = r.shard[0];
+        p.tile_list = (const int32_t*)r.tiles;
+        p.tile_count = r.count;
+        p.lane_cost = (uint32_t*)cost_dev;
+        CHECK(rt_render(&p, rt_scene_gpu(r.scene), nullptr));
+        std::vector<uint32_t> cost((size_t)slots);
+        CHECK(rt_memcpy_d2h(cost.data(), cost_dev, cost.size() * 4));  // synchronising copy
+        CHECK(rt_memcpy_d2d(r.rng, rng_copy, (size_t)slots * 48));
+        CHECK(rt_memset(r.shard[0], 0, shard_bytes));
+        std::vector<int32_t> map((size_t)rt_lane_plan_capacity(slots));
+        int64_t nlong = 0;
+        r.lanes = rt_lane_plan(cost.data(), slots, 48000.0, 1.0, map.data(), (int64_t)map.size(), &nlong);
+        if (r.lanes <= 0) CHECK(1);
+        CHECK(rt_malloc(&r.lane_map, (size_t)r.lanes * 4));
+        CHECK(rt_memcpy_h2d(r.lane_map, map.data(), (size_t)r.lanes * 4));
+        rt_free(rng_copy);
+        rt_free(cost_dev);
     }
     CHECK(rt_set_device(0));
     void *gathered = nullptr, *surface = nullptr, *lists_dev = nullptr;
@@ -127,6 +157,8 @@ static int run_split(const char* path, int w, int h, int frames, const char* ass
             p.out_shard = r.shard[f & 1];
             p.tile_list = (const int32_t*)r.tiles;
             p.tile_count = r.count;
+            p.lane_slots = (const int32_t*)r.lane_map;
+            p.lane_slot_count = r.lanes;
             CHECK(rt_render(&p, rt_scene_gpu(r.scene), nullptr));
         }
         CHECK(rt_comm_group_start());
@@ -152,6 +184,7 @@ static int run_split(const char* path, int w, int h, int frames, const char* ass
         rt_free(r.tiles);
         rt_free(r.shard[0]);
         rt_free(r.shard[1]);
+        rt_free(r.lane_map);
         rt_scene_destroy(r.scene);
         CHECK(rt_comm_destroy(comms[d]));
     }
