@@ -199,7 +199,7 @@ def pmc_pass(args, out_dir, timeout_s=150):
         cmd = [rocprof, "--kernel-trace", "--pmc", *cs, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
                sys.executable, os.path.abspath(__file__), "--pmc-child", "--config", args.config,
                "--plan", args.plan, "--tune", str(args.tune), "--refill", str(args.refill),
-               "--lanes", args.lanes, "--lane-units", str(args.lane_units)]
+               "--lanes", args.lanes, "--lane-units", str(args.lane_units), "--occupancy", str(args.occupancy_chosen)]
         try:
             r = subprocess.run(cmd, cwd=tempfile.gettempdir(), capture_output=True, text=True, timeout=timeout_s,
                                env=dict(os.environ, TMPDIR=tempfile.gettempdir()))
@@ -412,8 +412,13 @@ def run(args):
             rt.render(target, cur, prev, W, H, SPP, BOUNCES, i, tile_list=tile_list, tune=args.tune,
                       lane_slots=lane_slots, **refill(kw))
 
+    occupancy = {"waves_per_simd": 0 if args.occupancy == "auto" else int(args.occupancy)}
+
     def refill(kw):  # the probe (lane_cost) runs without refill
-        return kw if "lane_cost" in kw or args.foreign else dict(kw, refill_lanes=args.refill)
+        if "lane_cost" in kw:
+            return kw
+        kw = dict(occupancy, **kw)
+        return kw if args.foreign else dict(kw, refill_lanes=args.refill)
 
     # lane plan (rt_lane_plan): split the waves whose pixels form the frame's serial tail
     lanes_on = args.lanes == "on" or (args.lanes == "auto" and sharded)
@@ -423,6 +428,27 @@ def run(args):
                                               tile_list.numel() * 256, args.lane_units, dev)
         setup_s += time.perf_counter() - t1
         plan_info = dict(plan_info or {}, lanes=lane_info)
+
+    # occupancy (rt_render_params.waves_per_simd): time one untimed frame at 5 and at 6 waves per
+    # SIMD (twice each, on a copy of the RNG states) and keep the faster
+    if args.occupancy == "auto" and not args.pmc_child:
+        t1 = time.perf_counter()
+        rng_saved = rng.clone()
+        best = {}
+        for wps in (5, 6, 5, 6):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            render(0, bufs[0], None, waves_per_simd=wps)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            rng.copy_(rng_saved)
+            best[wps] = min(best.get(wps, 1e30), e0.elapsed_time(e1))
+        del rng_saved
+        occupancy["waves_per_simd"] = min(best, key=best.get)
+        setup_s += time.perf_counter() - t1
+        plan_info = dict(plan_info or {}, occupancy={"waves_per_simd": occupancy["waves_per_simd"],
+                                                     "probe_ms": {str(k): round(v, 3) for k, v in best.items()}})
+    args.occupancy_chosen = occupancy["waves_per_simd"] or 5
 
     if args.pmc_child:  # under rocprofv3 --pmc: a warm-up and two frames of the production kernel
         for i in range(3):
@@ -642,6 +668,8 @@ def main():
                          "longest-processing-time deal over ranks) or round-robin in row-major order")
     ap.add_argument("--refill", type=int, default=0,
                     help="rt_render refill_lanes: a wave refills this many idle lanes from the frame's queue (0 = off)")
+    ap.add_argument("--occupancy", default="auto", choices=["auto", "5", "6"],
+                    help="rt_render waves_per_simd; auto = time one untimed frame at each and keep the faster")
     ap.add_argument("--lanes", default="auto", choices=["auto", "on", "off"],
                     help="lane plan (rt_lane_plan: split the waves of the frame's costliest pixels); auto = on for N > 1")
     ap.add_argument("--lane-units", type=float, default=48000.0,

@@ -67,7 +67,8 @@ class RenderParams(ctypes.Structure):
                 ("out_shard", ctypes.c_void_p), ("stats", ctypes.c_void_p), ("segment_counter", ctypes.c_void_p),
                 ("tile_list", ctypes.c_void_p), ("tile_count", ctypes.c_int64), ("wave_clock", ctypes.c_void_p),
                 ("tune", ctypes.c_uint32), ("lane_slots", ctypes.c_void_p), ("lane_slot_count", ctypes.c_int64),
-                ("lane_cost", ctypes.c_void_p), ("priority_waves", ctypes.c_int64), ("refill_lanes", ctypes.c_int32)]
+                ("lane_cost", ctypes.c_void_p), ("priority_waves", ctypes.c_int64), ("refill_lanes", ctypes.c_int32),
+                ("waves_per_simd", ctypes.c_int32)]
 
 
 assert ctypes.sizeof(GPUScene) == 136 and ctypes.sizeof(GPUMaterial) == 64
@@ -332,7 +333,8 @@ def init_rng_states(rng, width, height, seed, shard_index=0, shard_count=1, stre
 
 def render(scene, surface, last, width, height, spp, bounces, frame_index=0, shard_index=0, shard_count=1,
            out_shard=None, stats=None, segment_counter=None, stream=None, tracer="fast", tile_list=None,
-           wave_clock=None, tune=0, lane_slots=None, lane_cost=None, priority_waves=0, refill_lanes=0):
+           wave_clock=None, tune=0, lane_slots=None, lane_cost=None, priority_waves=0, refill_lanes=0,
+           waves_per_simd=0):
     """rt_render: one frame (or one shard of it) on `stream` (default: torch's current stream).
     tile_list: device int32 tensor of tile ids (a row of a sharding.Plan) instead of the
     round-robin deal; wave_clock: device int64 tensor [entries*4] receiving per-wave clocks;
@@ -356,6 +358,7 @@ def render(scene, surface, last, width, height, spp, bounces, frame_index=0, sha
         p.wave_clock = wave_clock.data_ptr()
     p.tune = int(tune)
     p.refill_lanes = int(refill_lanes)
+    p.waves_per_simd = int(waves_per_simd)
     p.surface = surface.data_ptr() if surface is not None else None
     p.surface_last_frame = last.data_ptr() if last is not None else None
     p.width, p.height = width, height

@@ -47,6 +47,7 @@ struct RenderArgs {
     long long entry_count;           // entries of the lane order (lane map length, or slot_count)
     unsigned long long* queue_head;  // refill: entries taken from the queue so far (zeroed per launch), or null
     int refill_lanes;                // refill: idle lanes that trigger a refill
+    int waves_per_simd;              // production tracer occupancy: 5 (default) or 6
     uint32_t* lane_cost;             // per-slot work of a probe frame (timing kernel), or null
     int priority_waves;              // lane map: waves below this index run at raised priority
     const int* gate;                 // foreign scenes: the kernel runs only if *gate == gate_value

@@ -143,14 +143,30 @@ __device__ __forceinline__ float4 ldc(ConstF4 p, uint32_t i) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
+// The traversal stack of one lane: node indices, the first SL entries in LDS (lane stride WAVE),
+// deeper ones in a private per-lane array (scratch memory).  Deep stacks are rare -- no ray of a
+// config-2 frame goes past 15 entries -- so a 16-entry LDS stack (4 KB per wave) costs nothing
+// and leaves registers, not LDS, as the occupancy limit.
+template <int SL>
+struct Stack {
+    uint32_t* lds;  // this lane's entry 0 (entry i at lds[i * WAVE])
+    uint32_t* ovf;  // entries SL, SL + 1, ...
+    __device__ __forceinline__ void put(int i, uint32_t v) const {
+        if (i < SL) lds[i * WAVE] = v;
+        else ovf[i - SL] = v;
+    }
+    __device__ __forceinline__ uint32_t get(int i) const { return i < SL ? lds[i * WAVE] : ovf[i - SL]; }
+};
+
 // Pop stack entries until one passes `tmin < closest` (the reference's pop-time test).  An
 // entry is a node index (lane stride WAVE in LDS); tmin is recomputed from the node with the same
 // slab arithmetic, so the decision is the reference's, at one word of LDS per entry.
-__device__ __forceinline__ bool pop(const float4* nodes4, uint32_t* stk, int& sp, const Ray& R, float best,
+template <class S>
+__device__ __forceinline__ bool pop(const float4* nodes4, const S& stk, int& sp, const Ray& R, float best,
                                     uint32_t& first, uint32_t& count) {
     while (sp > 0) {
         sp--;
-        const uint32_t idx = stk[sp * WAVE];
+        const uint32_t idx = stk.get(sp);
         const float4 lo = nodes4[2 * idx], hi = nodes4[2 * idx + 1];
         int cl = UNSURE;
         float te, tx;
@@ -176,8 +192,8 @@ __device__ __forceinline__ bool pop(const float4* nodes4, uint32_t* stk, int& sp
 // One inner-node step: both children (adjacent in the node array) tested, the right child
 // continued in registers, the left one continued or pushed, exactly as the reference's
 // push(first), push(first+1), pop order.  Returns false when the lane must pop.
-template <bool STATS, class C>
-__device__ __forceinline__ bool inner_step(const float4* nodes4, uint32_t* stk, int& sp, const Ray& R, float best,
+template <bool STATS, class S, class C>
+__device__ __forceinline__ bool inner_step(const float4* nodes4, const S& stk, int& sp, const Ray& R, float best,
                                            uint32_t& first, uint32_t& count, C& c) {
     const float4 l0 = nodes4[2 * first], l1 = nodes4[2 * first + 1];
     const float4 r0 = nodes4[2 * first + 2], r1 = nodes4[2 * first + 3];
@@ -202,7 +218,7 @@ __device__ __forceinline__ bool inner_step(const float4* nodes4, uint32_t* stk, 
     }
     if (rlt == YES) {
         if (okl == YES) {
-            stk[sp * WAVE] = first;
+            stk.put(sp, first);
             sp++;
         }
         first = __float_as_uint(r1.z), count = __float_as_uint(r1.w);
@@ -796,8 +812,8 @@ __device__ __forceinline__ bool trav_begin(const float4* nodes4, const Ray& R, c
 // One small step of a lane at a small leaf or an inner node; false when the traversal is over.
 // (Testing a small leaf in the same step as the inner node that entered it was measured slower:
 // 22.2 vs 20.6 ms, the extra divergence costs more than the saved iterations.)
-template <bool STATS, class C>
-__device__ __forceinline__ bool small_step(const float4* nodes4, const float4* tris, const float4* spairs, uint32_t* stk,
+template <bool STATS, class S, class C>
+__device__ __forceinline__ bool small_step(const float4* nodes4, const float4* tris, const float4* spairs, const S& stk,
                                            const Ray& R, Hit& h, Trav& T, C& c) {
     if (T.count > 0) {
         if (!STATS && spairs) {
@@ -908,10 +924,10 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
 // cooperative rounds); 1: pairs in the shared-leaf loop, scalar cooperative rounds; 2: scalar
 // records only.  MODE & 4: leaves with a leaf tree walk it (a statistics frame then counts the
 // reference's triangle tests plus the tree's own work).
-template <bool STATS, int MODE, class C>
+template <bool STATS, int MODE, class S, class C>
 __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, const float4* pairs,
                                       const float4* tree, const float4* ltris, const float4* flat,
-                                      const float4* spairs, uint32_t tune, uint32_t* stk, uint32_t* scratch,
+                                      const float4* spairs, uint32_t tune, const S& stk, uint32_t* scratch,
                                       const Ray& R, Hit& h, bool live, C& c) {
     Trav T{0, 0, 0};
     bool active = live && trav_begin<STATS>(nodes4, R, h, T, c);

@@ -531,7 +531,8 @@ __device__ __forceinline__ int xcd_block(uint32_t tune) {
 // the bounce limit, start its next sample -- so a lane only idles once its whole pixel is
 // done.  The per-pixel draw order (u, v, then 4 draws per hit) is the reference's.
 template <int STACK, bool STATS, int MODE>
-__device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* const stk, uint32_t* const scratch) {
+__device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfast::Stack<(STACK < 16 ? STACK : 16)>& stk,
+                                                 uint32_t* const scratch) {
     if (a.gate && *a.gate != a.gate_value) return;  // foreign scenes: the other tracer renders this frame
     const float4* nodes4 = reinterpret_cast<const float4*>(a.nodes);
     const float4* tris = reinterpret_cast<const float4*>(a.tris);
@@ -762,21 +763,35 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, uint32_t* 
 // 0 = _w5, the default; 1 = unconstrained; 2 = _w6).
 template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
-    __shared__ uint32_t stack_lds[STACK * WAVE];  // one word per entry (rt_fast.h pop)
+    constexpr int SL = STACK < 16 ? STACK : 16;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
+    __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
     __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
-    render_fast_body<STACK, STATS, MODE>(a, stack_lds + threadIdx.x, scratch_lds);
+    uint32_t ovf[STACK > SL ? STACK - SL : 1];
+    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds + threadIdx.x, ovf}, scratch_lds);
 }
 template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(5))) void render_fast_kernel_w5(RenderArgs a) {
-    __shared__ uint32_t stack_lds[STACK * WAVE];
+    constexpr int SL = STACK < 16 ? STACK : 16;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
+    __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
     __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
-    render_fast_body<STACK, STATS, MODE>(a, stack_lds + threadIdx.x, scratch_lds);
+    uint32_t ovf[STACK > SL ? STACK - SL : 1];
+    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds + threadIdx.x, ovf}, scratch_lds);
 }
 template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(6))) void render_fast_kernel_w6(RenderArgs a) {
-    __shared__ uint32_t stack_lds[STACK * WAVE];
+    constexpr int SL = STACK < 16 ? STACK : 16;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
+    __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
     __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
-    render_fast_body<STACK, STATS, MODE>(a, stack_lds + threadIdx.x, scratch_lds);
+    uint32_t ovf[STACK > SL ? STACK - SL : 1];
+    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds + threadIdx.x, ovf}, scratch_lds);
+}
+template <int STACK, bool STATS, int MODE>
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(7))) void render_fast_kernel_w7(RenderArgs a) {
+    constexpr int SL = STACK < 16 ? STACK : 16;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
+    __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
+    __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
+    uint32_t ovf[STACK > SL ? STACK - SL : 1];
+    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds + threadIdx.x, ovf}, scratch_lds);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -901,10 +916,13 @@ hipError_t launch_grid(K kernel, const RenderArgs& args, int waves, hipStream_t 
 
 template <int STACK, bool STATS, int MODE>
 hipError_t launch_fast_m(const RenderArgs& args, int waves, hipStream_t stream) {
-    // default: 5 waves per SIMD (96 VGPRs, a few cold spills; 4 % faster than the compiler's 126)
-    const uint32_t occ = (args.tune >> 9) & 3u;
+    // default: 5 waves per SIMD (96 VGPRs, a few cold spills; 4 % faster than the compiler's 126);
+    // rt_render_params.waves_per_simd = 6: 80 VGPRs.  RT_TUNE bits 9-10 (A/B) override: 1 = the
+    // compiler's own choice, 2 = 6, 3 = 7 waves per SIMD.
+    const uint32_t occ = ((args.tune >> 9) & 3u) ? ((args.tune >> 9) & 3u) : (args.waves_per_simd == 6 ? 2u : 0u);
     if (!STATS && occ == 0) return launch_grid(render_fast_kernel_w5<STACK, STATS, MODE>, args, waves, stream);
     if (!STATS && occ == 2) return launch_grid(render_fast_kernel_w6<STACK, STATS, MODE>, args, waves, stream);
+    if (!STATS && occ == 3) return launch_grid(render_fast_kernel_w7<STACK, STATS, MODE>, args, waves, stream);
     return launch_grid(render_fast_kernel<STACK, STATS, MODE>, args, waves, stream);
 }
 
@@ -1343,6 +1361,9 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     const int waves = p->lane_slots ? (int)(p->lane_slot_count / WAVE) : tiles * 4;  // production tracer's grid
     a.entry_count = (long long)waves * WAVE;
     if (p->refill_lanes < 0 || p->refill_lanes > 64) return set_error("rt_render: refill_lanes must be in [0, 64]");
+    if (p->waves_per_simd != 0 && p->waves_per_simd != 5 && p->waves_per_simd != 6)
+        return set_error("rt_render: waves_per_simd must be 0, 5 or 6");
+    a.waves_per_simd = p->waves_per_simd;
     a.refill_lanes = p->refill_lanes;
     // Every device buffer must cover what the launch touches: a short buffer would fault the GPU.
     {

@@ -193,6 +193,11 @@ typedef struct rt_render_params {
      * queue, and a wave takes the next n entries as soon as n of its lanes have finished their
      * pixels (waves that start less than half full keep their lanes to themselves). */
     int32_t refill_lanes;
+    /* Occupancy of the production tracer: 0 = the default (5 waves per SIMD, 96 registers);
+     * 6 = 6 waves per SIMD (80 registers, more spills) -- faster on some scenes (config 2: 16.2 vs
+     * 16.9 ms), slower on others (config 4: 95 vs 90 ms); bench.py picks it per configuration by
+     * timing one untimed probe frame of each.  Any other value is an error. */
+    int32_t waves_per_simd;
 } rt_render_params;
 
 /* Layout rule: with out_shard set, RNG state s and output s are compact in list order
