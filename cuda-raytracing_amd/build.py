@@ -101,9 +101,22 @@ def build_oracle(force=False):
     return ORACLE_LIB
 
 
+def build_reference_parts(force=False):
+    """oracle/_ref: the parts of the reference that compile from their own sources here (the
+    vendored glm behind oracle/ref_glm.cpp), when /root/reference is present -- a checker for
+    the oracle, test infrastructure only (oracle/build_ref.sh)."""
+    out = os.path.join(ORACLE_DIR, "_ref", "libref_glm.so")
+    deps = [os.path.join(ORACLE_DIR, "ref_glm.cpp"), os.path.join(ORACLE_DIR, "build_ref.sh")]
+    if not os.path.isdir("/root/reference/include/glm") or (not force and _newer(out, deps)):
+        return out if os.path.exists(out) else None
+    _run(["bash", os.path.join(ORACLE_DIR, "build_ref.sh")])
+    return out
+
+
 def build_all(force=False):
     build_product(force)
     build_oracle(force)
+    build_reference_parts(force)
     build_host_driver(force)
 
 

@@ -12,8 +12,15 @@
  *     its kernel would need stand-ins for cuda_runtime.h / curand_kernel.h, which the rules
  *     forbid), and it ships no tests, fixtures or golden outputs.  Parity against the
  *     reference's own outputs is therefore UNPINNED.
- *   - Partial pins: the XORWOW jump matrices are checked against rocrand's published table
- *     (same recurrence); the bunny mesh is the assimp 3.3 import (assets/bunny_mesh.bin).
+ *   - Partial pins: every glm operation this file restates (intersectRayTriangle,
+ *     intersectRaySphere, normalize / cross / dot / reflect / mix / min / max / clamp,
+ *     quat * vec3, the camera's quat / mat4_cast / translate / scale / perspectiveRH / inverse
+ *     chain, rotate, mat4 * vec4) is checked bit for bit against the reference's OWN vendored
+ *     glm 0.9.9.8 compiled here (oracle/ref_glm.cpp + oracle/build_ref.sh -> oracle/_ref/;
+ *     tests/test_oracle_glm.py, vectors in tests/golden/glm_vectors.npz); the XORWOW jump
+ *     matrices against rocrand's published table (same recurrence); the bunny mesh is the
+ *     assimp 3.3 import (assets/bunny_mesh.bin).  Still unpinned: curand's seeding constants,
+ *     the scene / BVH builder's control flow, the texture unit's filtering, CUDA's sinf/cosf.
  *   - Semantics restated: the reference's arithmetic in IEEE fp32 WITHOUT contraction
  *     (nvcc contracts by default; not reproducible), curand's published XORWOW seeding and
  *     uniform mapping, the RT deterministic sin/cos and cube sampler definitions.
@@ -717,6 +724,17 @@ static int sphere_hit(v3 o, v3 d, v3 c, float r2, float* dist) {
     return *dist > eps;
 }
 
+/* quat * vec3 (type_quat.inl:343-350), q = (w, x, y, z) */
+static v3 q_rotate(const float* q, v3 v) {
+    v3 qv = V(q[1], q[2], q[3]), uv = vcross(qv, v), uuv = vcross(qv, uv);
+    return vadd(v, vscale(vadd(vscale(uv, q[0]), uuv), 2.0f));
+}
+
+/* glm::clamp(c, vec3(0), vec3(50)) (main_raytracing.cu:153; func_common.inl clamp = min(max)) */
+static v3 vclamp050(v3 c) {
+    return V(gmin(gmax(c.x, 0.0f), 50.0f), gmin(gmax(c.y, 0.0f), 50.0f), gmin(gmax(c.z, 0.0f), 50.0f));
+}
+
 typedef struct {
     int hit; float dist; v3 pos, nrm; const OMaterial* mat;
 } OHit;
@@ -800,11 +818,7 @@ static v3 ray_color(const OScene* s, v3 ro, v3 rd, ORng* rng, int bounces, float
         } else {
             st->misses++;
             if (s->sky) {
-                /* quat * vec3 (type_quat.inl:343-350) */
-                v3 qv = V(q[1], q[2], q[3]), uv = vcross(qv, rd), uuv = vcross(qv, uv);
-                v3 dir = vadd(rd, vscale(vadd(vscale(uv, q[0]), uuv), 2.0f));
-                v3 c = cube_sample(s->sky, s->sky_n, dir);
-                c = V(gmin(gmax(c.x, 0.0f), 50.0f), gmin(gmax(c.y, 0.0f), 50.0f), gmin(gmax(c.z, 0.0f), 50.0f));
+                v3 c = vclamp050(cube_sample(s->sky, s->sky_n, q_rotate(q, rd)));
                 color = vadd(color, vmul(thr, c));
             }
             break;
@@ -891,4 +905,83 @@ int oracle_render_costs(const OScene* s, int width, int height, int spp, int bou
                         uint64_t* stats, uint32_t* costs) {
     return render_rows(s, width, height, spp, bounces, frame_index, seed, rng, last, out, row_begin, row_end, threads,
                        stats, costs);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* The glm pieces of the restatement, exported so tests/test_oracle_glm.py can pin them     */
+/* bit for bit against the reference's own vendored glm (oracle/ref_glm.cpp, built from   */
+/* /root/reference/include/glm by oracle/build_ref.sh).  Same signatures as ref_glm.cpp.  */
+/* ------------------------------------------------------------------------------------ */
+static v3 ldv(const float* p) { return V(p[0], p[1], p[2]); }
+static void stv(float* p, v3 v) { p[0] = v.x; p[1] = v.y; p[2] = v.z; }
+
+void oracle_glm_tri_batch(int64_t n, const float* o, const float* d, const float* v0, const float* v1, const float* v2,
+                          int32_t* hit, float* out) {
+    for (int64_t i = 0; i < n; i++) {
+        float bx = 0.0f, by = 0.0f, t = 0.0f;
+        hit[i] = tri_hit(ldv(o + 3 * i), vnorm(ldv(d + 3 * i)), ldv(v0 + 3 * i), ldv(v1 + 3 * i), ldv(v2 + 3 * i), &bx, &by, &t);
+        out[3 * i] = bx; out[3 * i + 1] = by; out[3 * i + 2] = t;
+    }
+}
+
+void oracle_glm_sphere_batch(int64_t n, const float* o, const float* d, const float* c, const float* r, int32_t* hit,
+                             float* dist) {
+    for (int64_t i = 0; i < n; i++) {
+        float t = 0.0f;
+        hit[i] = sphere_hit(ldv(o + 3 * i), vnorm(ldv(d + 3 * i)), ldv(c + 3 * i), r[i] * r[i], &t);
+        dist[i] = t;
+    }
+}
+
+void oracle_glm_vec_batch(int64_t n, const float* a, const float* b, const float* s, float* out) {
+    for (int64_t i = 0; i < n; i++) {
+        v3 x = ldv(a + 3 * i), y = ldv(b + 3 * i);
+        float* o = out + 18 * i;
+        stv(o, vnorm(x));
+        stv(o + 3, vcross(x, y));
+        o[6] = vdot(x, y);
+        stv(o + 7, vreflect(x, y));
+        stv(o + 10, vmix(x, y, s[i]));
+        o[13] = gmax(x.x, y.x);
+        o[14] = gmin(x.x, y.x);
+        stv(o + 15, vclamp050(x));
+    }
+}
+
+void oracle_glm_quat_rotate_batch(int64_t n, const float* q, const float* v, float* out) {
+    for (int64_t i = 0; i < n; i++) stv(out + 3 * i, q_rotate(q + 4 * i, ldv(v + 3 * i)));
+}
+
+/* Camera::Update (Scene.cpp:15-36) as o_camera computes it (fov 90) */
+int oracle_glm_camera(const float* pos, float ax, float ay, int w, int h, float* out) {
+    OScene* s = (OScene*)calloc(1, sizeof(OScene));
+    OCamera cam;
+    if (!s) return 1;
+    memcpy(s->cam_pos, pos, 12);
+    s->cam_ax = ax; s->cam_ay = ay;
+    o_camera(s, w, h, &cam);
+    free(s);
+    memcpy(out, cam.origin, 12); memcpy(out + 3, cam.horizontal, 12);
+    memcpy(out + 6, cam.vertical, 12); memcpy(out + 9, cam.llc, 12);
+    return 0;
+}
+
+static M4 m_load(const float* m) { M4 r; for (int c = 0; c < 4; c++) for (int k = 0; k < 4; k++) r.m[c][k] = m[4 * c + k]; return r; }
+static void m_store(M4 a, float* m) { for (int c = 0; c < 4; c++) for (int k = 0; k < 4; k++) m[4 * c + k] = a.m[c][k]; }
+
+void oracle_glm_trs(const float* pos, float angle, const float* axis, const float* scl, float* out) {
+    M4 m = m_translate(m_ident(), ldv(pos));
+    m = m_rotate(m, angle, ldv(axis));
+    m_store(m_scale(m, ldv(scl)), out);
+}
+
+void oracle_glm_inverse(const float* m, float* out) { m_store(m_inverse(m_load(m)), out); }
+
+void oracle_glm_mat_apply_batch(int64_t n, const float* m1, const float* m2, const float* p, float* out) {
+    M4 t = m_mul(m_load(m1), m_load(m2));
+    for (int64_t i = 0; i < n; i++) {
+        float v1[4] = {p[3 * i], p[3 * i + 1], p[3 * i + 2], 1.0f}, v0[4] = {p[3 * i], p[3 * i + 1], p[3 * i + 2], 0.0f}, o[4];
+        m_vec(&t, v1, o); out[6 * i] = o[0]; out[6 * i + 1] = o[1]; out[6 * i + 2] = o[2];
+        m_vec(&t, v0, o); out[6 * i + 3] = o[0]; out[6 * i + 4] = o[1]; out[6 * i + 5] = o[2];
+    }
 }
