@@ -31,4 +31,7 @@ small, big, total = int(v[16]), int(v[17]), int(v[18])
 print(json.dumps({"config": sys.argv[1] if len(sys.argv) > 1 else "cfg2", "wave_cycles_total": total,
                   "small_frac": round(small / total, 3), "big_frac": round(big / total, 3),
                   "rest_frac": round(1 - (small + big) / total, 3), "rounds_coop": int(v[19]), "rounds_shared": int(v[20]),
-                  "coop_rays": int(v[21]), "wave_small_iters": int(v[8]), "lane_small": int(v[9])}))
+                  "coop_rays": int(v[21]), "wave_small_iters": int(v[8]), "lane_small": int(v[9]),
+                  "tree_walk_frac": round(int(v[7]) / total, 3), "tree_cluster_frac": round(int(v[22]) / total, 3),
+                  "tree_tri_frac": round(int(v[23]) / total, 3), "tree_tests": int(v[14]), "wave_big_rounds": int(v[10]),
+                  "lane_big": int(v[11])}))
