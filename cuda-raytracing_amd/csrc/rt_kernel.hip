@@ -539,12 +539,9 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
     // this lane's pixel: slot k*256 + tid of the launch's list (k < 0: none)
     int x = 0, y = 0;
     bool pixel = false;
-    uint32_t slot = 0;  // < 2^30 (rt_render checks the list size)
+    size_t slot = 0;
+    rt_rng_state* rs = a.rng;
     rtm::Xorwow rng{0, 0, 0, 0, 0, 0};
-    // the lane's RNG state (recomputed where needed rather than kept live: registers)
-    auto rng_state = [&]() -> rt_rng_state* {
-        return a.rng + (a.out_shard ? (size_t)slot : (size_t)y * a.width + x);
-    };
     auto bind = [&](int k, int tid) {
         const int tile = k >= 0 ? shard_tile(a, k) : -1;
         int lx, ly;
@@ -552,11 +549,9 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
         x = (tile % a.tiles_x) * TILE + lx;
         y = (tile / a.tiles_x) * TILE + ly;
         pixel = tile >= 0 && x < a.width && y < a.height;
-        slot = (uint32_t)(k >= 0 ? k : 0) * (TILE * TILE) + (uint32_t)tid;
-        if (pixel) {
-            const rt_rng_state* rs = rng_state();
-            rng = rtm::Xorwow{rs->d, rs->v[0], rs->v[1], rs->v[2], rs->v[3], rs->v[4]};
-        }
+        slot = (size_t)(k >= 0 ? k : 0) * (TILE * TILE) + tid;
+        rs = a.rng + (a.out_shard ? slot : (size_t)(pixel ? y : 0) * a.width + (pixel ? x : 0));
+        if (pixel) rng = rtm::Xorwow{rs->d, rs->v[0], rs->v[1], rs->v[2], rs->v[3], rs->v[4]};
     };
     // entry i of the launch's lane order: the lane map, or slot i (wave i / 64 = 8x8 sub-tile)
     auto bind_entry = [&](long long i) {
@@ -578,7 +573,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
     Counters c;
     const rtm::f3 cam_o = ld3(a.cam.origin), cam_h = ld3(a.cam.horizontal), cam_v = ld3(a.cam.vertical),
                   cam_ll = ld3(a.cam.lower_left_corner);
-    float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f;  // alpha: every sample adds 1 (RGBA(color, 1))
+    float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f, acc_a = 0.0f;
     int sample = 0, bounce = 0;
     bool path = false;
     rtm::f3 ro = cam_o, rd = cam_o, color = rtm::mk(0, 0, 0), thr = rtm::mk(1, 1, 1);
@@ -601,7 +596,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
                         base + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                     if ((long long)i < qn) {
                         bind_entry(qbase + (long long)i);
-                        acc_r = acc_g = acc_b = 0.0f;
+                        acc_r = acc_g = acc_b = acc_a = 0.0f;
                         sample = 0;
                     }
                 }
@@ -622,6 +617,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
                 bounce = 0;
                 path = true;
                 if (a.bounces == 0) {  // an empty bounce loop: the sample contributes (0,0,0,1)
+                    acc_a += 1.0f;
                     sample++;
                     path = false;
                     continue;
@@ -630,7 +626,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
                 pixel = false;
                 // main_raytracing.cu:195-199
                 const float fs = (float)a.spp;
-                const rtm::f4 res{acc_r / fs, acc_g / fs, acc_b / fs, 1.0f};  // alpha spp / spp (then written as 1)
+                const rtm::f4 res{acc_r / fs, acc_g / fs, acc_b / fs, acc_a / fs};
                 const float lerp = a.frame_index > 0 ? 1.0f / (float)(a.frame_index + 1) : 1.0f;
                 float4 prev;
                 float4* out;
@@ -644,7 +640,6 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
                 }
                 const rtm::f4 o = rtm::mix4(rtm::f4{prev.x, prev.y, prev.z, prev.w}, res, lerp);
                 *out = make_float4(o.x, o.y, o.z, 1.0f);
-                rt_rng_state* rs = rng_state();
                 rs->d = rng.d;
                 rs->v[0] = rng.v0;
                 rs->v[1] = rng.v1;
@@ -694,6 +689,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
             acc_r += color.x;
             acc_g += color.y;
             acc_b += color.z;
+            acc_a += 1.0f;
             sample++;
             path = false;
         }

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 cp cuda-raytracing_amd/librt_hip.so cuda-raytracing_amd/variants/current.so.bak
 for rep in ${REPS:-1}; do
 for v in ${VARS:-old new}; do
-  cp "cuda-raytracing_amd/variants/v_$v.so" cuda-raytracing_amd/librt_hip.so
+  if [ "$v" = new ]; then cp cuda-raytracing_amd/variants/current.so.bak cuda-raytracing_amd/librt_hip.so; else cp "cuda-raytracing_amd/variants/v_$v.so" cuda-raytracing_amd/librt_hip.so; fi
   for c in ${CFGS:-cfg2}; do
     timeout -k 10 240 python bench.py --config $c --no-pmc --no-cpu-baseline --steps ${STEPS:-10} --warmup 2 ${BENCH_ARGS:-} > gpurun_out/var_${v}_$c.log 2>&1
     rc=$?
