@@ -88,18 +88,3 @@ def gather_shards(shard, rank, world, out=None):
         return out
     dist.gather(shard, None, dst=0)
     return None
-
-
-def unshard_host(shards, width, height, tile_lists=None):
-    """numpy restatement of rt_unshard / rt_unshard_tiles (test use): [world, per_shard*256, 4]
-    -> [H, W, 4]."""
-    world, n, c = shards.shape
-    per_shard = n // TILE_PIXELS
-    img = np.zeros((height, width, c), dtype=shards.dtype)
-    seen = np.zeros((height, width), dtype=np.int64)
-    for r in range(world):
-        xs, ys = slot_pixels(width, height, r, world, per_shard, None if tile_lists is None else tile_lists[r])
-        ok = xs >= 0
-        img[ys[ok], xs[ok]] = shards[r][ok]
-        np.add.at(seen, (ys[ok], xs[ok]), 1)
-    return img, seen

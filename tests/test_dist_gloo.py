@@ -21,6 +21,22 @@ import rt_testlib as T
 W, H = 72, 40  # ragged: neither side is a multiple of the 16-pixel tile
 
 
+def unshard_host(shards, width, height, tile_lists=None):
+    """numpy restatement of rt_unshard / rt_unshard_tiles (the checker of the gloo rehearsal):
+    [world, per_shard*256, 4] -> [H, W, 4]."""
+    sh = T.load_rt().sharding
+    world, n, c = shards.shape
+    per_shard = n // sh.TILE_PIXELS
+    img = np.zeros((height, width, c), dtype=shards.dtype)
+    seen = np.zeros((height, width), dtype=np.int64)
+    for r in range(world):
+        xs, ys = sh.slot_pixels(width, height, r, world, per_shard, None if tile_lists is None else tile_lists[r])
+        ok = xs >= 0
+        img[ys[ok], xs[ok]] = shards[r][ok]
+        np.add.at(seen, (ys[ok], xs[ok]), 1)
+    return img, seen
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -65,7 +81,7 @@ def _worker(rank, world, port, frame, result_q, plan):
         shard[ok] = frame[ys[ok], xs[ok]]
         got = sh.gather_shards(torch.from_numpy(shard), rank, world)
         if rank == 0:
-            img, seen = sh.unshard_host(got.numpy(), W, H, lists)
+            img, seen = unshard_host(got.numpy(), W, H, lists)
             result_q.put((img, seen))
         dist.barrier()
     finally:
