@@ -37,6 +37,9 @@ def probe(rt, scene, W, H, SPP, BOUNCES):
     return cost
 
 
+TUNE, WPS = 0, 0  # --tune / --wps
+
+
 def lane_map(rt, scene, W, H, SPP, BOUNCES, mine, rng, lane):
     """rt_lane_plan of this shard from one probe frame's per-pixel work (lane = (ratio, budget))."""
     rt.init_rng_tiles(rng, W, H, mine, bench.SEED)
@@ -82,7 +85,7 @@ def time_shard(rt, scene, W, H, SPP, BOUNCES, tiles, r, n, reps, lane=None):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         rt.render(scene, None, bufs[(i + 1) & 1], W, H, SPP, BOUNCES, i, r, n, out_shard=bufs[i & 1], tile_list=mine,
-                  lane_slots=lm, priority_waves=nlong)
+                  lane_slots=lm, priority_waves=nlong, tune=TUNE, waves_per_simd=WPS)
         e1.record()
         torch.cuda.synchronize()
         if i:
@@ -98,7 +101,11 @@ def main():
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--weak", action="store_true", help="the frame grows with N as in bench.py --scaling weak")
     ap.add_argument("--lanes", default="", help="lane plans to try, 'ratio:budget;...' (rt_lane_plan)")
+    ap.add_argument("--tune", type=lambda x: int(x, 0), default=0, help="diagnostic A/B knobs passed to rt_render")
+    ap.add_argument("--wps", type=int, default=0, help="rt_render waves_per_simd (0 = default)")
     args = ap.parse_args()
+    global TUNE, WPS
+    TUNE, WPS = args.tune, args.wps
     rt = G.load_package()
     scene_name, W0, H0, SPP, BOUNCES, _ = bench.CONFIGS[args.config]
     torch.cuda.set_device(0)
