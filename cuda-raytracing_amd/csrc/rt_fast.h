@@ -149,6 +149,7 @@ __device__ __forceinline__ float4 ldc(ConstF4 p, uint32_t i) {
 // and leaves registers, not LDS, as the occupancy limit.
 template <int SL>
 struct Stack {
+    static constexpr int LDS_ENTRIES = SL;
     uint32_t* lds;  // this lane's entry 0 (entry i at lds[i * WAVE])
     uint32_t* ovf;  // entries SL, SL + 1, ...
     __device__ __forceinline__ void put(int i, uint32_t v) const {
@@ -918,6 +919,180 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
     return waiting;
 }
 
+// ---------------------------------------------------------------------------------------
+// Lone-ray traversal.  When a single lane of the wave is still in the small phase (the others
+// are done or parked at big leaves -- the tail of a wave, and most of the time of the one-pixel
+// waves a lane plan makes for the costliest pixels), that lane's steps are a chain of dependent
+// loads at ~1.4 K cycles each.  Here the whole wave runs that one ray's DFS instead:
+//   * the node to visit and the ray are wave-uniform: children come in through scalar loads and
+//     the slab tests run once, on uniform operands;
+//   * the traversal stack is distributed over the lanes' registers -- lane j holds entry j:
+//     node index, the node's EXACT slab tmin (IntersectAABB's, computed when the entry arrives),
+//     first, count -- so a pop is a ballot of `j < sp && tmin_j < closest` and the highest such
+//     lane: the entries above it are exactly the ones the reference pops and rejects
+//     (main_raytracing.cu:45), with no reload;
+//   * a small leaf's triangles are tested one per lane against the entry `closest`, and the
+//     (t, index) lexicographic minimum is the sequential loop's result (coop_leaf); a NaN
+//     distance sends the leaf to the sequential loop.
+// Same visit order, same decisions, bit for bit.  The lone lane's LDS stack entries move into
+// the lanes on entry (only when they all live in LDS) and back on exit (a big leaf: the wave's
+// big-leaf round takes over).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bcastu(uint32_t v, int lane) { return (uint32_t)__builtin_amdgcn_readlane((int)v, lane); }
+
+template <int SL>
+__device__ __forceinline__ void lone_traverse(const float4* nodes4, const float4* tris, const Stack<SL>& stk, int r,
+                                              const Ray& R, Hit& h, Trav& T, bool& active) {
+    const int lane = (int)(threadIdx.x & 63u);
+    uint32_t* const col = stk.lds - lane + r;  // lane r's LDS stack column
+    int sp = (int)bcastu((uint32_t)T.sp, r);
+    uint32_t cf = bcastu(T.first, r), cc = bcastu(T.count, r);
+    Ray U;  // the lone ray, wave-uniform
+    U.o = bcast3(R.o, r), U.d = bcast3(R.d, r), U.nd = bcast3(R.nd, r), U.r = bcast3(R.r, r);
+    U.fast = __builtin_amdgcn_readlane(R.fast ? 1 : 0, r) != 0;
+    float best = bcast(h.best, r);
+    int kind = __builtin_amdgcn_readlane(h.kind, r);
+    uint32_t id = bcastu(h.id, r);
+    float bx = bcast(h.bx, r), by = bcast(h.by, r);
+    // the distributed stack: lane j = entry j (tmin filtered as in pop: e_exact = tmin is the
+    // IEEE slab value, else q' with relative error < 2^-22.9, decided by classify_lt)
+    uint32_t e_idx = 0, e_first = 0, e_count = 0;
+    float e_tmin = 0.0f;
+    bool e_exact = false;
+    if (lane < sp) {
+        e_idx = col[lane * WAVE];
+        const float4 lo = nodes4[2 * e_idx], hi = nodes4[2 * e_idx + 1];
+        float tx;
+        if (U.fast) {
+            slab_approx(U, lo, hi, &e_tmin, &tx);
+        } else {
+            slab_exact(U, lo, hi, &e_tmin, &tx);
+            e_exact = true;
+        }
+        e_first = __float_as_uint(hi.z), e_count = __float_as_uint(hi.w);
+    }
+    bool done = false;
+    for (;;) {
+        bool do_pop = false;
+        if (cc == 0) {
+            // inner node: both children (uniform), the reference's push(first), push(first + 1), pop
+            const f4v a0 = ((ConstF4)nodes4)[2 * cf], a1 = ((ConstF4)nodes4)[2 * cf + 1];
+            const f4v b0 = ((ConstF4)nodes4)[2 * cf + 2], b1 = ((ConstF4)nodes4)[2 * cf + 3];
+            const float4 l0 = make_float4(a0.x, a0.y, a0.z, a0.w), l1 = make_float4(a1.x, a1.y, a1.z, a1.w);
+            const float4 r0 = make_float4(b0.x, b0.y, b0.z, b0.w), r1 = make_float4(b1.x, b1.y, b1.z, b1.w);
+            // inner_step's filtered-exact decisions, on uniform operands
+            float tl = 0.0f, tlx = 0.0f, tr = 0.0f, trx = 0.0f;
+            int okl = UNSURE, okr = UNSURE, rlt = UNSURE;
+            if (U.fast) {
+                slab_approx(U, l0, l1, &tl, &tlx);
+                slab_approx(U, r0, r1, &tr, &trx);
+                okl = classify_ok(tl, tlx);
+                okr = classify_ok(tr, trx);
+                rlt = okr == YES ? classify_lt(tr, best) : NO;
+            }
+            bool exact_l = false;
+            if (__builtin_amdgcn_readfirstlane((okl == UNSURE || okr == UNSURE || rlt == UNSURE) ? 1 : 0)) {
+                slab_exact(U, l0, l1, &tl, &tlx);
+                slab_exact(U, r0, r1, &tr, &trx);
+                okl = (tlx >= tl && tlx > 0.0f) ? YES : NO;
+                okr = (trx >= tr && trx > 0.0f) ? YES : NO;
+                rlt = (okr == YES && tr < best) ? YES : NO;
+                exact_l = true;
+            }
+            if (__builtin_amdgcn_readfirstlane(rlt == YES ? 1 : 0)) {
+                if (__builtin_amdgcn_readfirstlane(okl == YES ? 1 : 0)) {
+                    if (lane == sp) {
+                        e_idx = cf, e_tmin = tl, e_exact = exact_l;
+                        e_first = __float_as_uint(l1.z), e_count = __float_as_uint(l1.w);
+                    }
+                    sp++;
+                }
+                cf = __float_as_uint(r1.z), cc = __float_as_uint(r1.w);
+            } else {
+                bool llt = false;
+                if (__builtin_amdgcn_readfirstlane(okl == YES ? 1 : 0)) {
+                    int cl = exact_l ? (tl < best ? YES : NO) : classify_lt(tl, best);
+                    if (__builtin_amdgcn_readfirstlane(cl == UNSURE ? 1 : 0)) {
+                        float te, tx;
+                        slab_exact(U, l0, l1, &te, &tx);
+                        cl = te < best ? YES : NO;
+                    }
+                    llt = __builtin_amdgcn_readfirstlane(cl == YES ? 1 : 0) != 0;
+                }
+                if (llt) cf = __float_as_uint(l1.z), cc = __float_as_uint(l1.w);
+                else do_pop = true;
+            }
+        } else if (cc <= (uint32_t)BIG) {
+            // small leaf: one triangle per lane against the entry `closest`, (t, index) minimum
+            float t = 0.0f, x = 0.0f, y = 0.0f;
+            bool nan = false, acc = false;
+            if ((uint32_t)lane < cc) {
+                const uint32_t i = cf + (uint32_t)lane;
+                acc = tri_accept(U.o, U.nd, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], best, &t, &x, &y, &nan);
+            }
+            if (__ballot(nan)) {  // the sequential loop (never taken for finite scenes)
+                if (lane == 0) {
+                    for (uint32_t i = cf; i < cf + cc; i++) {
+                        float tt, xx, yy;
+                        bool dummy = false;
+                        if (tri_accept(U.o, U.nd, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], best, &tt, &xx, &yy, &dummy)) {
+                            best = tt, kind = 2, bx = xx, by = yy, id = __float_as_uint(tris[3 * i + 2].y);
+                        }
+                    }
+                }
+                best = bcast(best, 0), kind = __builtin_amdgcn_readlane(kind, 0), id = bcastu(id, 0);
+                bx = bcast(bx, 0), by = bcast(by, 0);
+            } else if (__ballot(acc)) {
+                const uint32_t mk = __ockl_wfred_min_u32(acc ? tkey(t) : 0xffffffffu);
+                const uint32_t mi = __ockl_wfred_min_u32(acc && tkey(t) == mk ? (uint32_t)lane : 0xffffffffu);
+                const int wl = (int)mi;
+                best = bcast(t, wl), bx = bcast(x, wl), by = bcast(y, wl), kind = 2;
+                id = __float_as_uint(tris[3 * (cf + mi) + 2].y);
+            }
+            do_pop = true;
+        } else {
+            break;  // a big leaf: the wave's big-leaf round takes over
+        }
+        if (do_pop) {
+            // pop-time `tmin < closest` of every entry at once; an entry too close to call is
+            // re-tested with the IEEE slab (its node reloaded)
+            int cl = NO;
+            if (lane < sp) cl = e_exact ? (e_tmin < best ? YES : NO) : classify_lt(e_tmin, best);
+            if (__ballot(cl == UNSURE)) {
+                if (cl == UNSURE) {
+                    const float4 lo = nodes4[2 * e_idx], hi = nodes4[2 * e_idx + 1];
+                    float tx;
+                    slab_exact(U, lo, hi, &e_tmin, &tx);
+                    e_exact = true;
+                    cl = e_tmin < best ? YES : NO;
+                }
+            }
+            const unsigned long long m = __ballot(cl == YES);
+            if (!m) {
+                done = true;
+                sp = 0;
+                break;
+            }
+            const int j = 63 - __clzll((long long)m);
+            cf = bcastu(e_first, j), cc = bcastu(e_count, j);
+            sp = j;
+        }
+    }
+    // back to lane r: its traversal state, hit, and (when it stops at a big leaf) its stack
+    if (lane == r) {
+        T.first = cf, T.count = cc, T.sp = sp;
+        h.best = best, h.kind = kind, h.id = id, h.bx = bx, h.by = by;
+        active = !done;
+    }
+    if (!done) {
+        if (lane < sp && lane < SL) col[lane * WAVE] = e_idx;
+        for (int j = SL; j < sp; j++) {
+            const uint32_t v = bcastu(e_idx, j);
+            if (lane == r) stk.put(j, v);
+        }
+    }
+}
+
 // BVHRayHit for one lane (`live` = the lane has a segment to trace), every lane of the wave
 // calling.  Small steps run while any lane has one; big leaves wait until every lane is done
 // or waiting at one.  MODE & 3 -- 0: big leaves through pair records (shared-leaf loop and
@@ -945,6 +1120,17 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
             const unsigned long long mI = __ballot(inner), mL = __ballot(leafs);
             if (mI | mL) {
                 const uint32_t nI = (uint32_t)__popcll(mI), nL = (uint32_t)__popcll(mL);
+                if constexpr (!STATS) {
+                    // one lane left in the small phase: the whole wave runs its DFS (lone_traverse),
+                    // when its stack lives in LDS (RT_TUNE bit 26 turns this off)
+                    if (nI + nL == 1 && (tune & (1u << 26)) == 0) {
+                        const int r = __ffsll((long long)(mI | mL)) - 1;
+                        if (__builtin_amdgcn_readlane(T.sp, r) <= S::LDS_ENTRIES) {
+                            lone_traverse(nodes4, tris, stk, r, R, h, T, active);
+                            continue;
+                        }
+                    }
+                }
                 // leaf step when nL * 4 >= nI * (q + 1); q = 1 measured best (RT_TUNE bits 13-15: q + 1)
                 const uint32_t qv = (tune >> 13) & 7u, q = qv ? qv - 1u : 1u;
                 if (TIMING) c.w_small++, c.l_small += inner || leafs;
