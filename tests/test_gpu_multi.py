@@ -212,6 +212,35 @@ def test_refill_equals_full(rt, refill, mapped):
     assert np.array_equal(rng.cpu().numpy(), rng_full)
 
 
+@pytest.mark.parametrize("which", ["bunny", "bunny4"])
+def test_one_pixel_waves_equal_full(rt, which):
+    """A lane map with ONE pixel per wave: every traversal runs through the lone-ray path
+    (rt_fast.h lone_traverse: the whole wave on one ray, stack spread over the lanes) -- the frames
+    and the RNG progression equal the plain render bit for bit; also with the lone path switched
+    off (RT_TUNE bit 26), so both paths are pinned against each other."""
+    w, h, spp, bounces = 40, 24, 2, 6
+    full, rng_full = full_frames(rt, w, h, spp, bounces, 2, which)
+    s = scene(rt, w, h, which)
+    tiles = rt.sharding.tiles_total(w, h)
+    mine = torch.arange(tiles, dtype=torch.int32, device="cuda")
+    xs, ys = rt.sharding.slot_pixels(w, h, 0, 1, tiles, np.arange(tiles))
+    slots = np.flatnonzero(xs >= 0).astype(np.int32)
+    m = np.full((slots.size, 64), -1, dtype=np.int32)
+    m[:, 0] = slots
+    lm = torch.from_numpy(m.ravel()).cuda()
+    for tune in (0, 1 << 26):
+        rng = rt.alloc_rng(w * h)
+        rt.init_rng_states(rng, w, h, T.SEED)
+        s.upload(rng.data_ptr())
+        bufs = [rt.alloc_surface(w, h), rt.alloc_surface(w, h)]
+        for f in range(2):
+            rt.render(s, bufs[f & 1], bufs[(f + 1) & 1], w, h, spp, bounces, f, tile_list=mine, lane_slots=lm, tune=tune)
+        torch.cuda.synchronize()
+        got = rt.surface_view(bufs[1], w).cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), full.view(np.uint32)), f"{which} tune={tune}"
+        assert np.array_equal(rng.cpu().numpy(), rng_full)
+
+
 def test_lane_map_misuse_is_refused(rt):
     w, h = 64, 64
     s = scene(rt, w, h)

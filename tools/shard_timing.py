@@ -52,7 +52,7 @@ def lane_map(rt, scene, W, H, SPP, BOUNCES, mine, rng, lane):
         os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
         np.save(os.path.join(ROOT, "gpurun_out", f"lanecost_{os.environ['LANE_SAVE']}_{mine.numel()}_{int(mine[0])}.npy"), c)
     m, nlong = rt.lane_plan(c, lane[0], lane[1])
-    nlong = nlong if len(lane) < 3 or lane[2] else 0  # lane[2] == 0: no wave priority
+    nlong = int(lane[2]) if len(lane) >= 3 else nlong  # lane[2]: the number of leading waves at raised priority
     rt.init_rng_tiles(rng, W, H, mine, bench.SEED)
     lm = torch.from_numpy(m).cuda()
     if os.environ.get("LANE_DIAG"):  # which waves are the long ones under this plan
