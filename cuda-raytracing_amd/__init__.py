@@ -59,6 +59,12 @@ class GPUMaterial(ctypes.Structure):
                 ("_pad", ctypes.c_float)]
 
 
+class BuildOptions(ctypes.Structure):
+    """rt_build_options (rt_abi.h): exact-preserving speed knobs of the mirror / BVH builders."""
+    _fields_ = [("leaf_tree_min", ctypes.c_uint32), ("cut_clusters", ctypes.c_uint32), ("cluster_max", ctypes.c_uint32),
+                ("split_angle", ctypes.c_float), ("bvh_small", ctypes.c_uint32), ("host_bvh", ctypes.c_int32)]
+
+
 class RenderParams(ctypes.Structure):
     _fields_ = [("surface", ctypes.c_void_p), ("surface_last_frame", ctypes.c_void_p),
                 ("width", ctypes.c_int32), ("height", ctypes.c_int32), ("pitch", ctypes.c_uint64),
@@ -87,6 +93,8 @@ SIGNATURES = {
     "rt_unshard": (_I, [_P, _U64, _I, _I, _I, _P, ctypes.c_int64, _P]),
     "rt_shard_plan_capacity": (ctypes.c_int64, [_I, _I, _I]),
     "rt_shard_plan": (_I, [_I, _I, _I, _P, ctypes.c_int64, _P, _P]),
+    "rt_get_build_options": (None, [_P]),
+    "rt_set_build_options": (_I, [_P]),
     "rt_lane_plan_capacity": (ctypes.c_int64, [ctypes.c_int64]),
     "rt_lane_plan": (ctypes.c_int64, [_P, ctypes.c_int64, ctypes.c_double, ctypes.c_double, _P, ctypes.c_int64, _P]),
     "rt_init_rng_tiles": (_I, [_P, _I, _I, _P, ctypes.c_int64, _U32, _P]),
@@ -418,6 +426,24 @@ def shard_plan(width, height, shard_count, tile_cost=None):
     _check(lib().rt_shard_plan(width, height, shard_count, cost_ptr, cap, lists.ctypes.data, counts.ctypes.data),
            "rt_shard_plan")
     return lists, counts
+
+
+def build_options():
+    """Current rt_build_options (a BuildOptions)."""
+    o = BuildOptions()
+    lib().rt_get_build_options(ctypes.byref(o))
+    return o
+
+
+def set_build_options(**changes):
+    """rt_set_build_options with the given fields changed (no arguments: the defaults)."""
+    if not changes:
+        _check(lib().rt_set_build_options(None), "rt_set_build_options")
+        return
+    o = build_options()
+    for k, v in changes.items():
+        setattr(o, k, v)
+    _check(lib().rt_set_build_options(ctypes.byref(o)), "rt_set_build_options")
 
 
 def lane_plan(cost, parallel_units=24000.0, slack=1.0):

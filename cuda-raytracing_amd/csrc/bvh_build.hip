@@ -519,11 +519,9 @@ extern "C" int rt_bvh_build_device(const GPUVertex* vertices, uint32_t vertex_co
                                    uint32_t face_count, GPUBVHNode* nodes_out, uint32_t* face_indices_out,
                                    uint32_t* node_count_out, int* max_depth_out, void* stream) {
     hipStream_t st = (hipStream_t)stream;
-    static const uint32_t small = [] {
-        const char* e = std::getenv("RT_BVH_SMALL");  // tuning knob, <= SMALL
-        const uint32_t v = e ? (uint32_t)std::strtoul(e, nullptr, 0) : 16u;
-        return v < 2u ? 2u : (v > SMALL ? SMALL : v);
-    }();
+    rt_build_options opt;
+    rt_get_build_options(&opt);  // rt_build_options.bvh_small, 2..SMALL
+    const uint32_t small = opt.bvh_small < 2u ? 2u : (opt.bvh_small > SMALL ? SMALL : opt.bvh_small);
     if (!vertices || !faces || !nodes_out || !face_indices_out || face_count == 0)
         return fail("rt_bvh_build_device: bad arguments");
     const uint32_t n = face_count;

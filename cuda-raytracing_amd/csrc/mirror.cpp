@@ -92,19 +92,13 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
         uint32_t pf;
         std::memcpy(&pf, &lead[11], 4);
         if (pf) continue;  // two nodes sharing one leaf range
-        static const uint32_t tree_min = [] {
-            const char* e = std::getenv("RT_LEAF_TREE_MIN");  // tuning
-            return e ? (uint32_t)std::strtoul(e, nullptr, 0) : MIRROR_TREE_LEAF;
-        }();
-        if (nd.prim_count >= tree_min) {
-            static const LeafTreeParams prm = [] {
-                LeafTreeParams p;
-                const char* e = std::getenv("RT_CUT_CLUSTERS");  // tuning knobs
-                if (e) p.cut_clusters = std::min<uint32_t>(32u, (uint32_t)std::strtoul(e, nullptr, 0));
-                if ((e = std::getenv("RT_SPLIT_ANGLE"))) p.split_angle = std::strtod(e, nullptr);
-                if ((e = std::getenv("RT_CLUSTER_MAX"))) p.cluster_max = std::min<uint32_t>(kClusterMax, (uint32_t)std::strtoul(e, nullptr, 0));
-                return p;
-            }();
+        rt_build_options opt;
+        rt_get_build_options(&opt);
+        if (nd.prim_count >= opt.leaf_tree_min) {
+            LeafTreeParams prm;
+            prm.cut_clusters = opt.cut_clusters;
+            prm.split_angle = opt.split_angle;
+            prm.cluster_max = opt.cluster_max;
             po = rt_build_leaf_tree(&out->tris[(size_t)nd.first_index * 12], nd.prim_count, prm, out->tree, out->ltris);
             rt_build_leaf_flat(out->tree, po, prm, out->flat);
             if (out->ltris.size() / 12 >= (1u << 26)) bad("leaf trees too large (record index >= 2^26)");
@@ -204,4 +198,41 @@ bool rt_internal_lookup_mirror(const GPUScene* s, MirrorDevice* out) {
     }
     *out = e.dev;
     return true;
+}
+
+// ---------------------------------------------------------------------------------------
+// Build options (rt_abi.h rt_build_options): process-wide, exact-preserving speed knobs.
+// ---------------------------------------------------------------------------------------
+namespace {
+std::mutex g_opt_mutex;
+rt_build_options default_options() {
+    rt_build_options o;
+    const LeafTreeParams p;
+    o.leaf_tree_min = MIRROR_TREE_LEAF;
+    o.cut_clusters = p.cut_clusters;
+    o.cluster_max = p.cluster_max;
+    o.split_angle = (float)p.split_angle;
+    o.bvh_small = 16;
+    o.host_bvh = 0;
+    return o;
+}
+rt_build_options g_options = default_options();
+}  // namespace
+
+extern "C" void rt_get_build_options(rt_build_options* out) {
+    if (!out) return;
+    std::lock_guard<std::mutex> lock(g_opt_mutex);
+    *out = g_options;
+}
+
+extern "C" int rt_set_build_options(const rt_build_options* o) {
+    const rt_build_options v = o ? *o : default_options();
+    if (v.leaf_tree_min < 2 || v.cut_clusters < 1 || v.cut_clusters > 32 || v.cluster_max < 1 || v.cluster_max > kClusterMax ||
+        !(v.split_angle >= 0.0f && v.split_angle < 3.2f) || v.bvh_small < 2 || v.bvh_small > 64 || (v.host_bvh != 0 && v.host_bvh != 1)) {
+        rt_internal_set_error("rt_set_build_options: value out of range");
+        return 1;
+    }
+    std::lock_guard<std::mutex> lock(g_opt_mutex);
+    g_options = v;
+    return 0;
 }

@@ -301,12 +301,14 @@ void Scene::BuildHost() {
 }
 
 // Geometry at least this large builds its BVH on the GPU (rt_bvh_build_device, byte-identical to
-// BVH::Calculate; 4-7x faster on the BASELINE scenes); RT_HOST_BVH=1 keeps the host builder.
+// BVH::Calculate; 4-7x faster on the BASELINE scenes); rt_build_options.host_bvh keeps the host builder.
 static constexpr size_t kGpuBvhMinFaces = 65536;
 
 // Scene.cpp:182-234
 void Scene::Upload(void* rng) {
-    static const bool host_bvh = std::getenv("RT_HOST_BVH") != nullptr;
+    rt_build_options opt;
+    rt_get_build_options(&opt);
+    const bool host_bvh = opt.host_bvh != 0;
     bool gpu_bvh = IsFlagDirty(DirtyFlagValue::BVH) && faces.size() >= kGpuBvhMinFaces && !host_bvh;
     if (gpu_bvh) {
         // vertices and faces first, then the build reads them on the device

@@ -402,6 +402,22 @@ size_t rt_scene_host_arrays(const rt_scene* scene, const GPUBVHNode** nodes, siz
                             size_t* vertex_count, const GPUFace** faces);
 int rt_scene_bvh_max_depth(const rt_scene* scene);
 
+/* Build options (process-wide; affect later rt_scene_upload / mirror builds and
+ * rt_bvh_build_device calls).  None of them changes a rendered bit -- the leaf trees and the GPU
+ * BVH builder are exact -- only speed; they replace environment knobs so that nothing in the
+ * shipped path reads the environment.  rt_get_build_options fills the current values (defaults
+ * on first use); rt_set_build_options(NULL) restores the defaults. */
+typedef struct rt_build_options {
+    uint32_t leaf_tree_min;   /* leaves with at least this many triangles get a leaf tree (1024) */
+    uint32_t cut_clusters;    /* leaf trees: clusters per subtree of the flat cut, 1..32 (32) */
+    uint32_t cluster_max;     /* leaf trees: triangles per tree leaf, 1..16 (16) */
+    float split_angle;        /* leaf trees: split by normals while the cone half-angle exceeds this, rad (0.03) */
+    uint32_t bvh_small;       /* GPU BVH builder: nodes this small build their subtree in one thread, 2..64 (16) */
+    int32_t host_bvh;         /* 1: rt_scene_upload always builds the BVH on the host (0: GPU from 65,536 faces) */
+} rt_build_options;
+void rt_get_build_options(rt_build_options* out);
+int rt_set_build_options(const rt_build_options* options);  /* 0, or an error for out-of-range values */
+
 /* The reference's BVH builder (BVH::Calculate, RayTracing/BVH.cpp:8-124) run on the GPU over
  * device arrays: nodes and face indices byte-identical to the host builder (depth-first node
  * numbering, the swap partition's permutation including failed axes).  nodes_out holds
