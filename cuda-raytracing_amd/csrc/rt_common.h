@@ -60,11 +60,13 @@ struct RenderArgs {
     const float4* ltris;  // their triangle records
     const float4* spairs; // small leaves' triangles in packed pairs, pair (i, i+1) at record i, or null
     const float4* flat;   // leaf trees' flat cluster / cut lists (leaftree.h) or null
-    uint32_t tune;  // diagnostic A/B knobs (rt_render_params.tune, 0 in production; see rt_fast.h / rt_kernel.hip for the rest: bits 12-15
-                    // split steps, 16-19 XCD run length (rt_kernel.hip xcd_block), 30 per-lane leaf-tree
-                    // walk, 31 subtree order):
-                    // bit0 no cooperative leaf rounds, bit1 no pair
-                    // records, bit2 no leaf trees, bit3 no small-leaf pairs, bits 4-5 big-leaf mode (rt_kernel.hip launch_fast_t)
+    // Diagnostic A/B knobs (rt_render_params.tune; 0 = the production path, every setting exact):
+    //   bit 0 no cooperative leaf rounds, 1 no pair records, 2 no leaf trees, 3 no small-leaf pairs,
+    //   4-5 big-leaf mode (launch_fast_t), 7 statistics through the leaf trees, 8 timing frame (phase
+    //   clocks), 9-10 occupancy override (1 compiler's choice, 2 = 6, 3 = 7 waves per SIMD),
+    //   11 per-wave clock records, 12 no split small steps, 13-15 split threshold, 16-19 XCD run
+    //   length (xcd_block), 26 no lone-ray traversal, 30 per-lane leaf-tree walk, 31 subtree order.
+    uint32_t tune;
 };
 
 struct Counters {
