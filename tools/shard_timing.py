@@ -37,7 +37,7 @@ def probe(rt, scene, W, H, SPP, BOUNCES):
     return cost
 
 
-TUNE, WPS = 0, 0  # --tune / --wps
+TUNE, WPS, SPLIT = 0, 0, 1  # --tune / --wps / --split
 
 
 def lane_map(rt, scene, W, H, SPP, BOUNCES, mine, rng, lane):
@@ -79,6 +79,11 @@ def time_shard(rt, scene, W, H, SPP, BOUNCES, tiles, r, n, reps, lane=None):
     rt.init_rng_tiles(rng, W, H, mine, bench.SEED)
     scene.upload(rng.data_ptr())
     lm, nlong = lane_map(rt, scene, W, H, SPP, BOUNCES, mine, rng, lane) if lane else (None, 0)
+    if SPLIT > 1:  # every 8x8 wave split into SPLIT waves of 64 / SPLIT pixels (rows of the sub-tile)
+        slots = np.arange(len(tiles) * 256, dtype=np.int32).reshape(-1, SPLIT, 64 // SPLIT)
+        m = np.full((slots.shape[0] * SPLIT, 64), -1, dtype=np.int32)
+        m[:, : 64 // SPLIT] = slots.reshape(-1, 64 // SPLIT)
+        lm, nlong = torch.from_numpy(m.ravel()).cuda(), 0
     bufs = [torch.zeros((len(tiles) * 256, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
     ms = []
     for i in range(reps + 1):
@@ -103,9 +108,10 @@ def main():
     ap.add_argument("--lanes", default="", help="lane plans to try, 'ratio:budget;...' (rt_lane_plan)")
     ap.add_argument("--tune", type=lambda x: int(x, 0), default=0, help="diagnostic A/B knobs passed to rt_render")
     ap.add_argument("--wps", type=int, default=0, help="rt_render waves_per_simd (0 = default)")
+    ap.add_argument("--split", type=int, default=1, help="split every 8x8 wave into this many waves (1, 2, 4)")
     args = ap.parse_args()
-    global TUNE, WPS
-    TUNE, WPS = args.tune, args.wps
+    global TUNE, WPS, SPLIT
+    TUNE, WPS, SPLIT = args.tune, args.wps, args.split
     rt = G.load_package()
     scene_name, W0, H0, SPP, BOUNCES, _ = bench.CONFIGS[args.config]
     torch.cuda.set_device(0)
