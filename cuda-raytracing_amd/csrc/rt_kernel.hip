@@ -568,7 +568,8 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
     // refill_lanes takes that many entries with one atomic (ballot + mbcnt rank the idle lanes), so
     // lanes stay busy until the queue drains instead of idling once their own pixel is done.
     // Waves that start less than half full (split waves of a lane plan) are not refilled.
-    bool drained = a.queue_head == nullptr || __popcll(__ballot(pixel)) < 32;
+    constexpr bool REFILL = (MODE & 64) != 0;  // refill is compiled into its own kernel variants only
+    bool drained = !REFILL || a.queue_head == nullptr || __popcll(__ballot(pixel)) < 32;
     const long long qbase = (long long)gridDim.x * WAVE;
     Counters c;
     const rtm::f3 cam_o = ld3(a.cam.origin), cam_h = ld3(a.cam.horizontal), cam_v = ld3(a.cam.vertical),
@@ -904,9 +905,9 @@ int resident_waves(K kernel) {
 }
 
 template <class K>
-hipError_t launch_grid(K kernel, const RenderArgs& args, int waves, hipStream_t stream) {
+hipError_t launch_grid(K kernel, const RenderArgs& args, int waves, bool refill, hipStream_t stream) {
     int grid = waves;
-    if (args.queue_head) {  // refill: one grid of resident waves, the rest through the queue
+    if (refill && args.queue_head) {  // refill variants: one grid of resident waves, the rest through the queue
         const int res = resident_waves(kernel);
         if (res > 0) grid = std::min(waves, res);
     }
@@ -920,10 +921,11 @@ hipError_t launch_fast_m(const RenderArgs& args, int waves, hipStream_t stream) 
     // rt_render_params.waves_per_simd = 6: 80 VGPRs.  RT_TUNE bits 9-10 (A/B) override: 1 = the
     // compiler's own choice, 2 = 6, 3 = 7 waves per SIMD.
     const uint32_t occ = ((args.tune >> 9) & 3u) ? ((args.tune >> 9) & 3u) : (args.waves_per_simd == 6 ? 2u : 0u);
-    if (!STATS && occ == 0) return launch_grid(render_fast_kernel_w5<STACK, STATS, MODE>, args, waves, stream);
-    if (!STATS && occ == 2) return launch_grid(render_fast_kernel_w6<STACK, STATS, MODE>, args, waves, stream);
-    if (!STATS && occ == 3) return launch_grid(render_fast_kernel_w7<STACK, STATS, MODE>, args, waves, stream);
-    return launch_grid(render_fast_kernel<STACK, STATS, MODE>, args, waves, stream);
+    constexpr bool refill = (MODE & 64) != 0;  // only these variants drain a refill queue
+    if (!STATS && occ == 0) return launch_grid(render_fast_kernel_w5<STACK, STATS, MODE>, args, waves, refill, stream);
+    if (!STATS && occ == 2) return launch_grid(render_fast_kernel_w6<STACK, STATS, MODE>, args, waves, refill, stream);
+    if (!STATS && occ == 3) return launch_grid(render_fast_kernel_w7<STACK, STATS, MODE>, args, waves, refill, stream);
+    return launch_grid(render_fast_kernel<STACK, STATS, MODE>, args, waves, refill, stream);
 }
 
 // Per-(device, stream) queue counter of refill launches, zeroed on the stream before each launch.
@@ -958,6 +960,8 @@ hipError_t launch_fast_t(const RenderArgs& args, int waves, hipStream_t stream) 
     // MODE bit 4: inner-node and small-leaf steps in separate iterations (rt_fast.h trace);
     // RT_TUNE bit 12 turns it off (A/B)
     const bool split = (args.tune & 4096u) == 0;
+    if (args.queue_head)  // refill (rt_render_params.refill_lanes): its own variants
+        return args.tree ? launch_fast_m<STACK, STATS, 85>(args, waves, stream) : launch_fast_m<STACK, STATS, 81>(args, waves, stream);
     if (args.tree) return split ? launch_fast_m<STACK, STATS, 21>(args, waves, stream)
                                 : launch_fast_m<STACK, STATS, 5>(args, waves, stream);
     const uint32_t mode = (args.tune >> 4) & 3u;
