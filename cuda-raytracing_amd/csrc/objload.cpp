@@ -17,7 +17,12 @@
 // (assets/bunny_mesh.bin, tests/test_objload.py): positions, vertex order and indices are
 // bit-identical; normals agree to a few ulps (|d| <= 3e-7) -- the summation order of the
 // smoothed normals follows assimp's std::sort of tied SpatialSort entries, which is not
-// reproduced bit for bit (parity of the normals unpinned below 4 ulps).
+// reproduced bit for bit (parity of the normals unpinned below 4 ulps).  Measured: 24,065 of
+// the 34,886 joined normals differ, and every differing one equals the normalised sum of the
+// same face normals (same angle-filtered set, same division normalisation) in some other
+// order (brute force over the orders); the per-corner import order is identical to assimp's.
+// Neither ascending/descending corner order, nor a stable sort, nor other plane-distance
+// roundings (FMA, double, unnormalised plane) reproduce assimp's tie order.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
