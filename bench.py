@@ -289,6 +289,20 @@ def setup_dist(backend, same_device):
     return rank, world
 
 
+def sanitize_wave_clocks(clocks):
+    """Per-wave s_memtime deltas (int64 view of the kernel's unsigned deltas) -> float64 costs and
+    the number of invalid entries.  A delta can come out negative when the wave was
+    context-switched between processes sharing the GPU (--same-device; seen once in a 2-rank
+    rehearsal); its cost is unknown, so it counts as the mean of the measured ones --
+    rt_shard_plan rejects costs < 0."""
+    c = np.asarray(clocks, dtype=np.int64).astype(np.float64)
+    bad = c < 0
+    if bad.any():
+        good = c[~bad]
+        c[bad] = good.mean() if good.size else 1.0
+    return c, int(bad.sum())
+
+
 def make_plan(rt, scene, W, H, SPP, BOUNCES, rank, world, plan_kind, dev):
     """(tile_lists [world, cap] int32 numpy, counts, probe info).  'cost': every rank renders its
     round-robin tiles once with per-wave clocks (set-up, untimed, throw-away RNG), the per-tile
@@ -311,8 +325,12 @@ def make_plan(rt, scene, W, H, SPP, BOUNCES, rank, world, plan_kind, dev):
               wave_clock=clocks)
     torch.cuda.synchronize()
     probe_s = time.perf_counter() - t0
+    per_wave, nbad = sanitize_wave_clocks(clocks.cpu().numpy())
+    if nbad:
+        print(f"[rank {rank}] probe frame: {nbad} of {per_wave.size} wave clocks invalid, replaced by the mean",
+              file=sys.stderr)
     cost = np.zeros(rt.sharding.tiles_total(W, H), dtype=np.float64)
-    cost[rr[rank, : rc[rank]]] = clocks.view(-1, 4).sum(1).double().cpu().numpy()
+    cost[rr[rank, : rc[rank]]] = per_wave.reshape(-1, 4).sum(1)
     if world > 1:
         t = torch.from_numpy(cost).to(dev) if dist.get_backend() == "nccl" else torch.from_numpy(cost)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)

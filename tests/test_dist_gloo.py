@@ -180,3 +180,22 @@ def test_shard_plan_rejects_bad_costs():
     cost[3] = -1.0
     with pytest.raises(rt.RTError):
         rt.shard_plan(64, 64, 2, cost)
+
+
+def test_wave_clock_sanitizer_feeds_a_valid_plan():
+    """bench.py's probe-frame clocks: a wrapped (negative) per-wave delta -- a wave context-switched
+    between two ranks sharing one GPU -- becomes the mean of the valid ones, so rt_shard_plan
+    (which rejects costs < 0) still deals the tiles."""
+    import bench
+
+    rt = T.load_rt()
+    tiles = rt.sharding.tiles_total(64, 64)
+    clocks = np.arange(1, 4 * tiles + 1, dtype=np.int64) * 1000
+    clocks[5] = -(1 << 40)
+    c, nbad = bench.sanitize_wave_clocks(clocks)
+    assert nbad == 1 and (c >= 0).all()
+    assert c[5] == np.delete(clocks, 5).astype(np.float64).mean()
+    ok, n0 = bench.sanitize_wave_clocks(clocks[6:])
+    assert n0 == 0 and np.array_equal(ok, clocks[6:].astype(np.float64))
+    lists, counts = rt.shard_plan(64, 64, 2, c.reshape(-1, 4).sum(1))
+    assert sorted(np.concatenate([lists[r, : counts[r]] for r in range(2)]).tolist()) == list(range(tiles))
