@@ -114,6 +114,17 @@ def weak_size(width, height, world):
     return w, int(round(w * height / width))
 
 
+def cpu_baseline_child(cfg, sample_rows=None, timeout_s=300):
+    """cpu_baseline in a fresh child process (no torch, no HIP runtime in it): the oracle's OpenMP
+    threads then share the box's CPU quota with nothing of the benchmark process."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--config", cfg,
+           "--cpu-rows", str(sample_rows or 0)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
+    if r.returncode != 0:
+        return {"error": f"exit {r.returncode}: {r.stderr[-300:]}"}
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def cpu_baseline(cfg, sample_rows=None):
     """Oracle ("port") on this host's cores: bounded sample of the same frame (rows)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -133,8 +144,12 @@ def cpu_baseline(cfg, sample_rows=None):
     _, st = osc.render(w, h, spp, bounces, rng=rng, rows=(r0, r1), threads=threads, stats=True)
     dt = time.perf_counter() - t
     samples = (r1 - r0) * w * spp
+    try:
+        load = open("/proc/loadavg").read().split()[:3]
+    except OSError:
+        load = None
     return {"value": round(float(st[0]) / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "cpu": cpu_model(), "host_threads": os.cpu_count(),
+            "cpu": cpu_model(), "host_threads": os.cpu_count(), "host_loadavg": load, "process": "child (oracle only)",
             "sample": f"{cfg} rows [{r0},{r1}) of {h} ({samples} camera samples, {int(st[0])} segments), {dt:.1f} s",
             "samples_per_s": round(samples / dt, 1)}
 
@@ -150,30 +165,67 @@ def _free_port():
     return port
 
 
-def launch_ranks(n):
+def launch_ranks(n, cmd=None, deadline_s=480.0, poll_s=0.05):
     """bench.py --gpus N without a launcher: start N rank processes of this script (RANK /
-    LOCAL_RANK / WORLD_SIZE / MASTER_* set), forward rank 0's stdout, return the first failing
-    exit code (and stop the other ranks then)."""
+    LOCAL_RANK / WORLD_SIZE / MASTER_* set), forward rank 0's stdout, and return the first failing
+    exit code (stopping the other ranks then: a dead rank leaves the others waiting in a
+    collective).  A job still running after `deadline_s` -- a rank stuck in communicator set-up or
+    in a collective -- is killed whole: the ranks still alive are named on stderr and the launcher
+    returns 124.  The launcher itself never touches the GPU."""
     port = _free_port()
-    procs = []
+    cmd = cmd or [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    procs = {}
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
-                                      stdout=None if r == 0 else subprocess.DEVNULL))
+        procs[r] = subprocess.Popen(cmd, env=env, stdout=None if r == 0 else subprocess.DEVNULL)
+    t0 = time.monotonic()
     rc = 0
     while procs:
-        for p in list(procs):
+        for r, p in list(procs.items()):
             code = p.poll()
             if code is None:
                 continue
-            procs.remove(p)
+            del procs[r]
             if code != 0 and rc == 0:
                 rc = code
-                for q in procs:  # a dead rank leaves the others waiting in a collective
+                print(f"bench.py launcher: rank {r} exited with {code}; stopping ranks {sorted(procs)}", file=sys.stderr)
+                for q in procs.values():
                     q.kill()
-        time.sleep(0.05)
+        if procs and deadline_s and time.monotonic() - t0 > deadline_s:
+            print(f"bench.py launcher: ranks {sorted(procs)} still running after {deadline_s:.0f} s; killing all ranks",
+                  file=sys.stderr, flush=True)
+            for q in procs.values():
+                q.kill()
+            for q in procs.values():
+                q.wait()
+            return 124
+        time.sleep(poll_s)
     return rc
+
+
+class Watchdog:
+    """Per-rank deadline for N > 1 jobs under any launcher (torch.distributed.run has none of its
+    own): if the rank is still running after `deadline_s`, it names the phase it is stuck in and
+    ends its process with 124, which ends the job (the other ranks fail their next collective or
+    hit their own deadline)."""
+
+    def __init__(self, rank, deadline_s):
+        import threading
+
+        self.rank, self.phase = rank, "start"
+        self.timer = threading.Timer(deadline_s, self._fire) if deadline_s else None
+        if self.timer:
+            self.timer.daemon = True
+            self.timer.start()
+
+    def _fire(self):
+        print(f"bench.py rank {self.rank}: deadline exceeded in phase '{self.phase}'; exiting", file=sys.stderr, flush=True)
+        os._exit(124)
+
+    def cancel(self):
+        if self.timer:
+            self.timer.cancel()
 
 
 # ------------------------------------------------------------------------------------------
@@ -200,6 +252,8 @@ def pmc_pass(args, out_dir, timeout_s=150):
                sys.executable, os.path.abspath(__file__), "--pmc-child", "--config", args.config,
                "--plan", args.plan, "--tune", str(args.tune), "--refill", str(args.refill),
                "--lanes", args.lanes, "--lane-units", str(args.lane_units), "--occupancy", str(args.occupancy_chosen)]
+        if args.foreign:
+            cmd.append("--foreign")
         try:
             r = subprocess.run(cmd, cwd=tempfile.gettempdir(), capture_output=True, text=True, timeout=timeout_s,
                                env=dict(os.environ, TMPDIR=tempfile.gettempdir()))
@@ -289,17 +343,28 @@ def setup_dist(backend, same_device):
     return rank, world
 
 
-def sanitize_wave_clocks(clocks):
-    """Per-wave s_memtime deltas (int64 view of the kernel's unsigned deltas) -> float64 costs and
-    the number of invalid entries.  A delta can come out negative when the wave was
-    context-switched between processes sharing the GPU (--same-device; seen once in a 2-rank
-    rehearsal); its cost is unknown, so it counts as the mean of the measured ones --
-    rt_shard_plan rejects costs < 0."""
+CLOCK_HZ = 100e6  # wave_clock ticks: the device's constant 100 MHz clock (s_memrealtime)
+
+
+def sanitize_wave_clocks(clocks, wall_s=None, k=4096.0):
+    """Per-wave probe clocks (int64 view of the kernel's unsigned s_memrealtime deltas) -> float64
+    costs and the number of entries flagged invalid.  The clock is the device's one 100 MHz time
+    base, so a valid delta lies in [0, probe wall time]; this stays as a guard that logs: a delta
+    that is negative, longer than the probe frame's wall time (`wall_s`, when given), or more than
+    `k` x the median of the others is replaced by that median (rt_shard_plan rejects costs < 0,
+    and an inflated outlier would pull a mean up).  k is far above any real spread: a sky-only wave
+    and the heaviest floor wave of config 3 differ by a few hundred times."""
     c = np.asarray(clocks, dtype=np.int64).astype(np.float64)
     bad = c < 0
+    if wall_s is not None:
+        bad |= c > wall_s * CLOCK_HZ * 1.05 + 1e3
+    if (~bad).any():
+        med = float(np.median(c[~bad]))
+        if med > 0:
+            bad |= c > k * med
     if bad.any():
         good = c[~bad]
-        c[bad] = good.mean() if good.size else 1.0
+        c[bad] = float(np.median(good)) if good.size else 1.0
     return c, int(bad.sum())
 
 
@@ -325,19 +390,22 @@ def make_plan(rt, scene, W, H, SPP, BOUNCES, rank, world, plan_kind, dev):
               wave_clock=clocks)
     torch.cuda.synchronize()
     probe_s = time.perf_counter() - t0
-    per_wave, nbad = sanitize_wave_clocks(clocks.cpu().numpy())
+    per_wave, nbad = sanitize_wave_clocks(clocks.cpu().numpy(), wall_s=probe_s)
     if nbad:
-        print(f"[rank {rank}] probe frame: {nbad} of {per_wave.size} wave clocks invalid, replaced by the mean",
+        print(f"[rank {rank}] probe frame: {nbad} of {per_wave.size} wave clocks invalid, replaced by the median",
               file=sys.stderr)
     cost = np.zeros(rt.sharding.tiles_total(W, H), dtype=np.float64)
     cost[rr[rank, : rc[rank]]] = per_wave.reshape(-1, 4).sum(1)
     if world > 1:
-        t = torch.from_numpy(cost).to(dev) if dist.get_backend() == "nccl" else torch.from_numpy(cost)
+        both = np.concatenate([cost, [float(nbad)]])
+        t = torch.from_numpy(both).to(dev) if dist.get_backend() == "nccl" else torch.from_numpy(both)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        cost = t.cpu().numpy()
+        both = t.cpu().numpy()
+        cost, nbad = both[:-1], int(both[-1])
     lists, counts = rt.shard_plan(W, H, world, cost)
     del rng, shard, clocks
-    return lists, counts, {"probe_frame_s": round(probe_s, 4), "kind": "cost (probe-frame wave clocks, LPT)"}
+    return lists, counts, {"probe_frame_s": round(probe_s, 4), "kind": "cost (probe-frame wave clocks, LPT)",
+                           "invalid_wave_clocks": nbad}
 
 
 def make_lane_map(rt, render, rng, slots, units, dev):
@@ -364,7 +432,11 @@ def run(args):
     import torch.distributed as dist
     import __graft_entry__ as G
 
+    multi = int(os.environ.get("WORLD_SIZE", "1")) > 1
+    wd = Watchdog(int(os.environ.get("RANK", "0")), args.rank_deadline if multi else 0)
+    wd.phase = "rendezvous"
     rank, world = setup_dist(args.backend, args.same_device)
+    wd.phase = "scene set-up and plans"
     assert world == args.gpus or args.pmc_child, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     rt = G.load_package()
     scene_name, W, H, SPP, BOUNCES, desc = CONFIGS[args.config]
@@ -462,10 +534,17 @@ def run(args):
             rng.copy_(rng_saved)
             best[wps] = min(best.get(wps, 1e30), e0.elapsed_time(e1))
         del rng_saved
+        if world > 1:
+            # one variant for the whole job: every rank takes the setting whose slowest rank is fastest
+            cdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+            t = torch.tensor([best[5], best[6]], dtype=torch.float64, device=cdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            best = {5: float(t[0]), 6: float(t[1])}
         occupancy["waves_per_simd"] = min(best, key=best.get)
         setup_s += time.perf_counter() - t1
         plan_info = dict(plan_info or {}, occupancy={"waves_per_simd": occupancy["waves_per_simd"],
-                                                     "probe_ms": {str(k): round(v, 3) for k, v in best.items()}})
+                                                     "probe_ms": {str(k): round(v, 3) for k, v in best.items()},
+                                                     "agreed": "max over ranks" if world > 1 else "single rank"})
     args.occupancy_chosen = occupancy["waves_per_simd"] or 5
 
     if args.pmc_child:  # under rocprofv3 --pmc: a warm-up and two frames of the production kernel
@@ -528,12 +607,14 @@ def run(args):
             if rank == 0:
                 rt.unshard_tiles(frame, W, H, got, lists_dev)
 
+    wd.phase = "warm-up frames"
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
     if sharded:
         dist.barrier()
     torch.cuda.synchronize()
+    wd.phase = "timed frames"
     t_start = time.perf_counter()
     for i in range(args.warmup, n_total):
         step(i)
@@ -543,6 +624,7 @@ def run(args):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
 
+    wd.phase = "report"
     segs = int(seg_counter.item())
     kern_ms = [ev[i][0].elapsed_time(ev[i][1]) for i in range(args.warmup, n_total)]
     kern_avg_s = float(np.mean(kern_ms)) / 1e3
@@ -614,7 +696,7 @@ def run(args):
             result["check_equal"] = check_unsharded(rt, scene_name, W, H, SPP, BOUNCES, n_total, final)
         if world == 1 and not args.no_cpu_baseline:
             auto_rows = {"cfg1": 256, "cfg2": 1080, "cfg3": 64, "cfg4": 540, "cfg5": 1080}[args.config]
-            result["cpu_baseline"] = cpu_baseline(args.config, args.cpu_rows or auto_rows)
+            result["cpu_baseline"] = cpu_baseline_child(args.config, args.cpu_rows or auto_rows)
         print(json.dumps(result), flush=True)
     if comm is not None:
         torch.cuda.synchronize()
@@ -622,6 +704,7 @@ def run(args):
     if sharded:
         dist.barrier()
         dist.destroy_process_group()
+    wd.cancel()
     return 0
 
 
@@ -696,13 +779,19 @@ def main():
     ap.add_argument("--foreign", action="store_true",
                     help="render a GPUScene filled outside this library (the reference's Scene::Upload pattern): "
                          "fingerprint-gated mirror, no host synchronisation per frame")
+    ap.add_argument("--rank-deadline", type=float, default=480.0,
+                    help="N > 1: seconds after which a still-running job is killed whole (0 = none)")
     ap.add_argument("--check", action="store_true",
                     help="after timing, rank 0 re-renders the same frames unsharded and compares the final frame")
+    ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.cpu_baseline_child:  # the CPU baseline's own process (see cpu_baseline_child)
+        print(json.dumps(cpu_baseline(args.config, args.cpu_rows or None)), flush=True)
+        return 0
     if args.plan is None:
         args.plan = "cost"
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.pmc_child:
-        return launch_ranks(args.gpus)
+        return launch_ranks(args.gpus, deadline_s=args.rank_deadline)
     return run(args)
 
 

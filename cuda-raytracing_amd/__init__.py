@@ -446,7 +446,7 @@ def set_build_options(**changes):
     _check(lib().rt_set_build_options(ctypes.byref(o)), "rt_set_build_options")
 
 
-def lane_plan(cost, parallel_units=24000.0, slack=1.0):
+def lane_plan(cost, parallel_units=48000.0, slack=1.0):
     """rt_lane_plan: (int32 numpy lane map, number of leading long waves) from per-slot work
     (numpy uint32/int32 [slots], a probe frame's lane_cost)."""
     cost = np.ascontiguousarray(np.asarray(cost).astype(np.uint32))

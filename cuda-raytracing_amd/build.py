@@ -28,7 +28,9 @@ ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 # fp32 division and square root (bit-exact agreement between host code, kernels and oracle).
 FP_FLAGS = ["-ffp-contract=off", "-fno-fast-math"]
 HOST_SOURCES = ["scene.cpp", "objload.cpp", "mirror.cpp", "leaftree.cpp", "xorwow.cpp", "image.cpp", "shard.cpp"]
-HIP_SOURCES = ["rt_kernel.hip", "image.hip", "bvh_build.hip", "comm.hip"]
+# the render kernel families compile as separate translation units, in parallel (rt_render.h)
+HIP_SOURCES = ["rt_fast_prod.hip", "rt_fast_timing.hip", "rt_fast_ab.hip", "rt_fast_ab2.hip", "rt_fast_refill.hip",
+               "rt_fast_stats.hip", "rt_ref.hip", "rt_kernel.hip", "image.hip", "bvh_build.hip", "comm.hip"]
 
 
 def _run(cmd):
@@ -53,6 +55,7 @@ def build_product(force=False):
     if not force and _newer(LIB, deps):
         return LIB
     jobs = []
+    headers = _deps(CSRC, (".h",)) + _deps(INC, (".h",)) + [os.path.abspath(__file__)]
     for src in HIP_SOURCES:
         obj = os.path.join(BUILD, src + ".o")
         jobs.append((obj, [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *FP_FLAGS,
@@ -65,8 +68,10 @@ def build_product(force=False):
     # translation units compile in parallel (the render kernel's dominates)
     from concurrent.futures import ThreadPoolExecutor
     workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 8))
+    # an object is rebuilt when its source or any header changed
+    stale = [j for j in jobs if force or not _newer(j[0], [j[1][j[1].index("-c") + 1]] + headers)]
     with ThreadPoolExecutor(max_workers=workers) as ex:
-        list(ex.map(lambda j: _run(j[1]), jobs))
+        list(ex.map(lambda j: _run(j[1]), stale))
     objs = [o for o, _ in jobs]
     tmp = LIB + ".tmp"
     _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-L/opt/rocm/lib", "-lrccl", "-o", tmp])

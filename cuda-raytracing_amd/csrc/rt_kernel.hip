@@ -1,14 +1,14 @@
-// rt_kernel.hip -- MI355X (gfx950) render path behind the C-ABI of include/rt_abi.h.
+// rt_kernel.hip -- MI355X (gfx950) render path behind the C-ABI of include/rt_abi.h: the memory /
+// cube-map shim, rt_render (argument checks, foreign-scene gating, the choice of kernel variant),
+// the RNG set-up and the multi-GPU unshard.
 //
-// Kernels
-//   render_kernel<STACK, STATS>  per-pixel path tracer (RayTracing/main_raytracing.cu:33-200):
-//       one 256-thread workgroup per 16x16 pixel tile, each wave64 an 8x8 sub-tile (ray
-//       coherence inside a wave), per-thread BVH stack in LDS laid out [entry][thread] so
-//       the 64 lanes of a push/pop hit 64 consecutive dwords (conflict-free), RNG state in
-//       registers for the whole pixel (one 24-B read and one 24-B write per pixel instead
-//       of a global read-modify-write per draw).
+// Kernels here
 //   init_rng_kernel              curand_init(seed, pixel, 0) with GF(2) jump matrices.
 //   unshard_kernel               scatter gathered tile shards back into a pitched surface.
+//   fingerprint_kernel (+ gate)  content fingerprint of a foreign scene's arrays, per frame.
+// The render kernels live in their own translation units (rt_render.h): rt_fast_*.hip (the
+// production tracer, rt_fast_body.h + rt_fast.h, per variant family) and rt_ref.hip (the
+// reference-layout and flat tracers).
 //
 // Numerics: compiled with -ffp-contract=off and IEEE fp32 division/sqrt, so every value
 // matches the CPU oracle bit for bit ("Parity").
@@ -125,675 +125,11 @@ static int cube_size(uint64_t handle) {
 // ---------------------------------------------------------------------------------------
 // render kernel
 // ---------------------------------------------------------------------------------------
+#include "rt_render.h"
+
 namespace {
 
 using namespace rtk;
-using rtfast::Hit;
-
-// The sphere loop of GetRayHit (main_raytracing.cu:88-103): strict `<` replaces.
-template <bool STATS>
-__device__ __forceinline__ void trace_spheres(const RenderArgs& a, rtm::f3 ro, rtm::f3 nd, Hit& h, Counters& c) {
-    for (int i = 0; i < a.sphere_count; i++) {
-        const GeometrySphere& sp = a.spheres[i];
-        float dist;
-        if (rtd::intersect_sphere(ro, nd, ld3(sp.position), sp.radius * sp.radius, &dist)) {
-            if (dist >= h.best) continue;
-            h.best = dist;
-            h.kind = 1;
-            h.id = (uint32_t)i;
-            if (STATS) c.sacc++;
-        }
-    }
-}
-
-// BVHRayHit (main_raytracing.cu:33-81) on the reference arrays, literally: uint32 stack,
-// pop, AABB test against the current closest distance, leaf -> face_indices -> faces ->
-// vertices, inner -> push first, first+1 (right child popped first).  Used for scenes
-// whose buffers were not uploaded through rt_scene_upload (no leaf-ordered mirror).
-struct RefTracer {
-    static constexpr int WORDS = 1;
-    template <int STACK, bool STATS>
-    __device__ static void trace(const RenderArgs& a, uint32_t* stk, rtm::f3 ro, rtm::f3 rd, rtm::f3 nd, Hit& h,
-                                 Counters& c) {
-        int sp = 0;
-        stk[0] = 0u;
-        sp = 1;
-        while (sp) {
-            const GPUBVHNode& node = a.nodes[stk[(--sp) * WAVE]];
-            if (STATS) c.node++;
-            if (!rtd::intersect_aabb(ro, rd, node.bmin, node.bmax, h.best)) continue;
-            if (node.prim_count > 0) {
-                for (uint32_t i = 0; i < node.prim_count; i++) {
-                    const uint32_t fi = a.face_indices[node.first_index + i];
-                    const GPUFace f = a.faces[fi];
-                    float bx, by, dist;
-                    if (STATS) c.tri++;
-                    if (rtd::intersect_triangle(ro, nd, ld3(a.vertices[f.v0].position), ld3(a.vertices[f.v1].position),
-                                                ld3(a.vertices[f.v2].position), &bx, &by, &dist)) {
-                        if (dist >= h.best || dist < 0.0f) continue;
-                        h.best = dist;
-                        h.kind = 2;
-                        h.id = fi;
-                        h.bx = bx;
-                        h.by = by;
-                        if (STATS) c.tacc++;
-                    }
-                }
-            } else {
-                stk[(sp++) * WAVE] = node.first_index;
-                stk[(sp++) * WAVE] = node.first_index + 1;
-            }
-        }
-    }
-};
-
-// The slab part of IntersectAABB (Math.h:50-61) that does not depend on the closest
-// distance: returns tmin and whether tmax >= tmin && tmax > 0.  The remaining clause,
-// tmin < ray_length, is evaluated when the reference would pop the node.
-__device__ __forceinline__ bool slab(rtm::f3 o, rtm::f3 d, float4 lo, float4 hi, float* tmin_out) {
-    // lo = (bmin.x, bmin.y, bmin.z, bmax.x), hi = (bmax.y, bmax.z, first, count)
-    float tx1 = (lo.x - o.x) / d.x, tx2 = (lo.w - o.x) / d.x;
-    float tmin = fminf(tx1, tx2), tmax = fmaxf(tx1, tx2);
-    float ty1 = (lo.y - o.y) / d.y, ty2 = (hi.x - o.y) / d.y;
-    tmin = fmaxf(tmin, fminf(ty1, ty2)), tmax = fminf(tmax, fmaxf(ty1, ty2));
-    float tz1 = (lo.z - o.z) / d.z, tz2 = (hi.y - o.z) / d.z;
-    tmin = fmaxf(tmin, fminf(tz1, tz2)), tmax = fminf(tmax, fmaxf(tz1, tz2));
-    *tmin_out = tmin;
-    return tmax >= tmin && tmax > 0;
-}
-
-// The same traversal, re-associated for the GPU without changing a single decision:
-//  * siblings are adjacent (children of an inner node at first, first+1), so an inner node
-//    loads both children (64 contiguous bytes) and runs both slab tests at once; the right
-//    child -- the one the reference pops next -- continues in registers, the left child is
-//    pushed with its tmin, and `tmin < closest` is checked when it is popped, against the
-//    closest distance at that moment, exactly as the reference's pop-time test;
-//  * leaves read the leaf-ordered FlatTri mirror (one 48-byte record per test instead of
-//    the index -> face -> 3 vertex dependent-load chain);
-//  * node visit order, tested triangles and their order, and every comparison are the
-//    reference's, so the closest hit (including ties between coincident faces) is identical.
-// Stack entries: (node index, tmin bits) in LDS, [entry][lane].
-struct FlatTracer {
-    static constexpr int WORDS = 2;
-    template <int STACK, bool STATS>
-    __device__ static void trace(const RenderArgs& a, uint32_t* stk, rtm::f3 ro, rtm::f3 rd, rtm::f3 nd, Hit& h,
-                                 Counters& c) {
-        const float4* nodes4 = reinterpret_cast<const float4*>(a.nodes);
-        // root (node 0), tested against the closest sphere distance
-        float4 lo = nodes4[0], hi = nodes4[1];
-        float tmin;
-        if (STATS) c.node++;
-        if (!slab(ro, rd, lo, hi, &tmin) || !(tmin < h.best)) return;
-        uint32_t first = __float_as_uint(hi.z), count = __float_as_uint(hi.w);
-        int sp = 0;
-        for (;;) {
-            if (count > 0) {
-                // leaf: the reference's per-triangle loop over face_indices[first .. first+count)
-                for (uint32_t i = first; i < first + count; i++) {
-                    const FlatTri t = a.tris[i];
-                    if (STATS) c.tri++;
-                    const rtm::f3 v0 = rtm::mk(t.a.x, t.a.y, t.a.z);
-                    const rtm::f3 e1 = rtm::mk(t.a.w, t.b.x, t.b.y);
-                    const rtm::f3 e2 = rtm::mk(t.b.z, t.b.w, t.c.x);
-                    float bx, by, dist;
-                    if (rtd::intersect_triangle_e(ro, nd, v0, e1, e2, &bx, &by, &dist)) {
-                        if (dist >= h.best || dist < 0.0f) continue;
-                        h.best = dist;
-                        h.kind = 2;
-                        h.id = __float_as_uint(t.c.y);
-                        h.bx = bx;
-                        h.by = by;
-                        if (STATS) c.tacc++;
-                    }
-                }
-            } else {
-                const float4 l0 = nodes4[2 * first], l1 = nodes4[2 * first + 1];
-                const float4 r0 = nodes4[2 * first + 2], r1 = nodes4[2 * first + 3];
-                if (STATS) c.node += 2;
-                float tl, tr;
-                const bool okl = slab(ro, rd, l0, l1, &tl);
-                const bool okr = slab(ro, rd, r0, r1, &tr);
-                if (okr && tr < h.best) {
-                    if (okl) {
-                        stk[(sp * 2) * WAVE] = first;
-                        stk[(sp * 2 + 1) * WAVE] = __float_as_uint(tl);
-                        sp++;
-                    }
-                    first = __float_as_uint(r1.z), count = __float_as_uint(r1.w);
-                    continue;
-                }
-                if (okl && tl < h.best) {
-                    first = __float_as_uint(l1.z), count = __float_as_uint(l1.w);
-                    continue;
-                }
-            }
-            // pop until an entry passes tmin < closest
-            bool found = false;
-            while (sp > 0) {
-                sp--;
-                const uint32_t idx = stk[(sp * 2) * WAVE];
-                const float t = __uint_as_float(stk[(sp * 2 + 1) * WAVE]);
-                if (t < h.best) {
-                    const float4 nh = nodes4[2 * idx + 1];
-                    first = __float_as_uint(nh.z), count = __float_as_uint(nh.w);
-                    found = true;
-                    break;
-                }
-            }
-            if (!found) break;
-        }
-    }
-};
-
-// The per-pixel path tracer: raytracing_kernel_main + ray_color (main_raytracing.cu:111-200).
-template <class Tracer, int STACK, bool STATS>
-__device__ __forceinline__ void shade_pixel(const RenderArgs& a, uint32_t* stk, int x, int y, size_t rng_index,
-                                            size_t out_slot, Counters& c) {
-    rt_rng_state* rs = a.rng + rng_index;
-    rtm::Xorwow rng{rs->d, rs->v[0], rs->v[1], rs->v[2], rs->v[3], rs->v[4]};
-    const rtm::f3 cam_o = ld3(a.cam.origin), cam_h = ld3(a.cam.horizontal), cam_v = ld3(a.cam.vertical),
-                  cam_ll = ld3(a.cam.lower_left_corner);
-    float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f, acc_a = 0.0f;
-
-    for (int sample = 0; sample < a.spp; sample++) {
-        // main_raytracing.cu:190: uv = (pixel + vec2(rng(), rng())) / vec2(W, H), u drawn first
-        const float ru = rng.uniform();
-        const float rv = rng.uniform();
-        const float uvx = ((float)x + ru) / (float)a.width;
-        const float uvy = ((float)y + rv) / (float)a.height;
-        // GPUCamera::GetRay (GPUScene.h:13): llc + u*h + v*v - origin (not normalized)
-        rtm::f3 ro = cam_o;
-        rtm::f3 rd = rtm::sub(rtm::add(rtm::add(cam_ll, rtm::muls(cam_h, uvx)), rtm::muls(cam_v, uvy)), cam_o);
-
-        rtm::f3 color = rtm::mk(0, 0, 0), thr = rtm::mk(1, 1, 1);
-        for (int bounce = 0; bounce < a.bounces; bounce++) {
-            c.seg++;
-            // GetRayHit (main_raytracing.cu:83-109)
-            const rtm::f3 nd = rtm::normalize(rd);
-            Hit h;
-            h.best = 1e30f;
-            h.kind = 0;
-            h.id = 0;
-            h.bx = h.by = 0.0f;
-            trace_spheres<STATS>(a, ro, nd, h, c);
-            Tracer::template trace<STACK, STATS>(a, stk, ro, rd, nd, h, c);
-
-            if (h.kind != 0) {
-                if (STATS) c.hit++;
-                // Attributes of the final closest hit (the reference recomputes them on every
-                // accept; only the last accept survives, so computing them once is identical).
-                const rtm::f3 pos = rtm::add(ro, rtm::muls(nd, h.best));
-                rtm::f3 nrm;
-                uint32_t mat;
-                if (h.kind == 1) {
-                    const GeometrySphere& sp = a.spheres[h.id];
-                    nrm = rtm::divs(rtm::sub(pos, ld3(sp.position)), sp.radius);
-                    mat = (uint32_t)sp.material;
-                } else {
-                    const GPUFace f = a.faces[h.id];
-                    const float bz = (1.0f - h.bx) - h.by;
-                    nrm = rtm::normalize(rtm::add(rtm::add(rtm::muls(ld3(a.vertices[f.v0].normal), h.bx),
-                                                           rtm::muls(ld3(a.vertices[f.v1].normal), h.by)),
-                                                  rtm::muls(ld3(a.vertices[f.v2].normal), bz)));
-                    if (rtm::dot(nd, nrm) >= 0.0f) nrm = rtm::neg(nrm);
-                    mat = f.material;
-                }
-                const GPUMaterial& m = a.materials[mat];
-                const float do_spec = (rng.uniform() < m.specular_percent) ? 1.0f : 0.0f;
-                color = rtm::add(color, rtm::mul(thr, ld3(m.emissive)));
-                const float om = 1.0f - do_spec;
-                thr = rtm::mul(thr, rtm::mk(m.albedo[0] * om + m.specular[0] * do_spec,
-                                            m.albedo[1] * om + m.specular[1] * do_spec,
-                                            m.albedo[2] * om + m.specular[2] * do_spec));
-                // GetRandomPointOnSphere (Random.h:23-46)
-                const float zz = rng.uniform() * 2.0f - 1.0f;
-                const float ang = rng.uniform() * 3.141592654f * 2.0f;
-                const float rr = sqrtf(1.0f - zz * zz);
-                const rtm::f3 sph = rtm::mk(rr * rtm::rt_cosf(ang), rr * rtm::rt_sinf(ang), zz);
-                const rtm::f3 diffuse = rtm::normalize(rtm::add(nrm, sph));
-                rtm::f3 spec = rtm::normalize(rtm::reflect(rd, nrm));
-                spec = rtm::normalize(rtm::mix(spec, diffuse, m.roughness * m.roughness));
-                const rtm::f3 ndir = rtm::normalize(rtm::add(rtm::muls(diffuse, om), rtm::muls(spec, do_spec)));
-                ro = rtm::add(pos, rtm::muls(nrm, 0.01f));
-                rd = ndir;
-                // Russian roulette (main_raytracing.cu:140-148)
-                const float p = rtm::gmax(thr.x, rtm::gmax(thr.y, thr.z));
-                if (rng.uniform() > p) break;
-                thr = rtm::muls(thr, 1.0f / p);
-            } else {
-                if (STATS) c.miss++;
-                if (a.sky) {
-                    const rtm::f3 dir = rtd::quat_rotate(a.qw, a.qx, a.qy, a.qz, rd);
-                    const rtm::f3 cs = rtd::cube_sample(a.sky, a.sky_n, dir);
-                    const rtm::f3 cl = rtm::mk(rtm::gmin(rtm::gmax(cs.x, 0.0f), 50.0f), rtm::gmin(rtm::gmax(cs.y, 0.0f), 50.0f),
-                                               rtm::gmin(rtm::gmax(cs.z, 0.0f), 50.0f));
-                    color = rtm::add(color, rtm::mul(thr, cl));
-                }
-                break;
-            }
-        }
-        acc_r += color.x;
-        acc_g += color.y;
-        acc_b += color.z;
-        acc_a += 1.0f;
-    }
-
-    // main_raytracing.cu:195-199
-    const float fs = (float)a.spp;
-    const rtm::f4 res{acc_r / fs, acc_g / fs, acc_b / fs, acc_a / fs};
-    const float lerp = a.frame_index > 0 ? 1.0f / (float)(a.frame_index + 1) : 1.0f;
-    float4 prev;
-    float4* out;
-    if (a.out_shard) {
-        prev = a.last ? reinterpret_cast<const float4*>(a.last)[out_slot] : make_float4(0, 0, 0, 0);
-        out = a.out_shard + out_slot;
-    } else {
-        prev = a.last ? *reinterpret_cast<const float4*>(a.last + (size_t)y * a.pitch + (size_t)x * 16)
-                      : make_float4(0, 0, 0, 0);
-        out = reinterpret_cast<float4*>(a.surface + (size_t)y * a.pitch + (size_t)x * 16);
-    }
-    const rtm::f4 o = rtm::mix4(rtm::f4{prev.x, prev.y, prev.z, prev.w}, res, lerp);
-    *out = make_float4(o.x, o.y, o.z, 1.0f);
-
-    rs->d = rng.d;
-    rs->v[0] = rng.v0;
-    rs->v[1] = rng.v1;
-    rs->v[2] = rng.v2;
-    rs->v[3] = rng.v3;
-    rs->v[4] = rng.v4;
-}
-
-// One wave per workgroup; wave g renders the 8x8 sub-tile (g & 3) of shard tile (g >> 2).
-// The hardware dispatcher hands out the next sub-tile as soon as a wave retires, which
-// balances cheap (sky) against expensive (floor leaf) tiles.
-template <class Tracer, int STACK, bool STATS>
-__global__ __launch_bounds__(WAVE) void render_kernel(RenderArgs a) {
-    if (a.gate && *a.gate != a.gate_value) return;  // foreign scenes: the other tracer renders this frame
-    __shared__ uint32_t stack_lds[STACK * Tracer::WORDS * WAVE];
-    uint32_t* const stk = stack_lds + threadIdx.x;
-    const int g = (int)blockIdx.x;
-    const int k = g >> 2;
-    const int tid = ((g & 3) << 6) | (int)threadIdx.x;  // thread index within the 16x16 tile
-    const int tile = shard_tile(a, k);
-    int lx, ly;
-    tile_pixel(tid, &lx, &ly);
-    const int x = (tile % a.tiles_x) * TILE + lx;
-    const int y = (tile / a.tiles_x) * TILE + ly;
-    Counters c;
-    if (tile >= 0 && x < a.width && y < a.height) {  // off-frame lanes stay for the wave reduction
-        const size_t slot = (size_t)(k >= 0 ? k : 0) * (TILE * TILE) + tid;
-        const size_t rng_index = a.out_shard ? slot : (size_t)y * a.width + x;
-        shade_pixel<Tracer, STACK, STATS>(a, stk, x, y, rng_index, slot, c);
-    }
-    // Segment count (always on: the Mrays/s numerator), one atomic per wave.
-    if (a.seg_counter) {
-        unsigned long long v = c.seg;
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if (threadIdx.x == 0) atomicAdd(a.seg_counter, v);
-    }
-    if (STATS) {
-        atomicAdd(a.stats + RT_STAT_SEGMENTS, c.seg);
-        atomicAdd(a.stats + RT_STAT_NODES, c.node);
-        atomicAdd(a.stats + RT_STAT_TRI_TESTS, c.tri);
-        atomicAdd(a.stats + RT_STAT_TRI_ACCEPTS, c.tacc);
-        atomicAdd(a.stats + RT_STAT_SPHERE_ACCEPTS, c.sacc);
-        atomicAdd(a.stats + RT_STAT_HITS, c.hit);
-        atomicAdd(a.stats + RT_STAT_MISSES, c.miss);
-    }
-}
-
-// ray_color's per-segment tail (main_raytracing.cu:118-158) for the segment whose closest hit is
-// `h`: emission, throughput, the next direction from 4 draws, Russian roulette; or the sky on a
-// miss.  Updates the path (ro, rd, color, thr); returns true when the path ends here.
-template <bool STATS>
-__device__ __forceinline__ bool shade_segment(const RenderArgs& a, const rtfast::Hit& h, rtm::f3& ro, rtm::f3& rd,
-                                              const rtm::f3 nd, rtm::Xorwow& rng, rtm::f3& color, rtm::f3& thr,
-                                              Counters& c) {
-    bool end = false;
-    if (h.kind != 0) {
-        if (STATS) c.hit++;
-        const rtm::f3 pos = rtm::add(ro, rtm::muls(nd, h.best));
-        rtm::f3 nrm;
-        uint32_t mat;
-        if (h.kind == 1) {
-            const GeometrySphere& sp = a.spheres[h.id];
-            nrm = rtm::divs(rtm::sub(pos, ld3(sp.position)), sp.radius);
-            mat = (uint32_t)sp.material;
-        } else {
-            const GPUFace f = a.faces[h.id];
-            const float bz = (1.0f - h.bx) - h.by;
-            nrm = rtm::normalize(rtm::add(rtm::add(rtm::muls(ld3(a.vertices[f.v0].normal), h.bx),
-                                                   rtm::muls(ld3(a.vertices[f.v1].normal), h.by)),
-                                          rtm::muls(ld3(a.vertices[f.v2].normal), bz)));
-            if (rtm::dot(nd, nrm) >= 0.0f) nrm = rtm::neg(nrm);
-            mat = f.material;
-        }
-        const GPUMaterial& m = a.materials[mat];
-        const float do_spec = (rng.uniform() < m.specular_percent) ? 1.0f : 0.0f;
-        color = rtm::add(color, rtm::mul(thr, ld3(m.emissive)));
-        const float om = 1.0f - do_spec;
-        thr = rtm::mul(thr, rtm::mk(m.albedo[0] * om + m.specular[0] * do_spec,
-                                    m.albedo[1] * om + m.specular[1] * do_spec,
-                                    m.albedo[2] * om + m.specular[2] * do_spec));
-        // GetRandomPointOnSphere (Random.h:23-46)
-        const float zz = rng.uniform() * 2.0f - 1.0f;
-        const float ang = rng.uniform() * 3.141592654f * 2.0f;
-        const float rr = sqrtf(1.0f - zz * zz);
-        const rtm::f3 sph = rtm::mk(rr * rtm::rt_cosf(ang), rr * rtm::rt_sinf(ang), zz);
-        const rtm::f3 diffuse = rtm::normalize(rtm::add(nrm, sph));
-        rtm::f3 spec = rtm::normalize(rtm::reflect(rd, nrm));
-        spec = rtm::normalize(rtm::mix(spec, diffuse, m.roughness * m.roughness));
-        const rtm::f3 ndir = rtm::normalize(rtm::add(rtm::muls(diffuse, om), rtm::muls(spec, do_spec)));
-        ro = rtm::add(pos, rtm::muls(nrm, 0.01f));
-        rd = ndir;
-        // Russian roulette (main_raytracing.cu:140-148)
-        const float p = rtm::gmax(thr.x, rtm::gmax(thr.y, thr.z));
-        if (rng.uniform() > p) {
-            end = true;
-        } else {
-            thr = rtm::muls(thr, 1.0f / p);
-        }
-    } else {
-        if (STATS) c.miss++;
-        if (a.sky) {
-            const rtm::f3 dir = rtd::quat_rotate(a.qw, a.qx, a.qy, a.qz, rd);
-            const rtm::f3 cs = rtd::cube_sample(a.sky, a.sky_n, dir);
-            const rtm::f3 cl = rtm::mk(rtm::gmin(rtm::gmax(cs.x, 0.0f), 50.0f), rtm::gmin(rtm::gmax(cs.y, 0.0f), 50.0f),
-                                       rtm::gmin(rtm::gmax(cs.z, 0.0f), 50.0f));
-            color = rtm::add(color, rtm::mul(thr, cl));
-        }
-        end = true;
-    }
-    return end;
-}
-
-// Logical sub-tile of this workgroup.  The dispatcher deals workgroups round-robin over the 8
-// XCDs (workgroup g -> XCD g % 8), so consecutive sub-tiles would land in different L2s.
-// Instead XCD x takes runs of S = 2^v consecutive sub-tiles: its i-th workgroup renders
-// sub-tile ((i / S) * 8 + x) * S + i % S (a permutation of the first multiple of 8S workgroups;
-// the rest keep their index), so neighbouring pixels share an L2.  v = 5 (runs of 8 tiles,
-// 128x16 px): config 2 18.29 -> 17.73 ms; v = 4 17.8, v = 6 18.1, v = 1-3 18.1-18.3.
-// RT_TUNE bits 16-19 override v; 15 keeps the dispatcher's order.
-__device__ __forceinline__ int xcd_block(uint32_t tune) {
-    const uint32_t g = blockIdx.x, tv = (tune >> 16) & 15u, v = tv ? tv : 5u;
-    if (v == 15u) return (int)g;
-    const uint32_t S = 1u << v, full = gridDim.x / (8u * S) * (8u * S);
-    if (g >= full) return (int)g;
-    const uint32_t i = g >> 3, x = g & 7u;
-    return (int)((((i / S) << 3) + x) * S + i % S);
-}
-
-// The production kernel: rt_fast.h traversal + a flat per-lane segment loop.
-// raytracing_kernel_main / ray_color (main_raytracing.cu:111-200) nest `for sample { for
-// bounce { ... break } }`; on a SIMD machine that makes every lane wait at the end of each
-// sample for the longest path of the wave.  Here each lane runs a small state machine --
-// start a camera sample, trace a segment, shade, end the path on a miss / Russian roulette /
-// the bounce limit, start its next sample -- so a lane only idles once its whole pixel is
-// done.  The per-pixel draw order (u, v, then 4 draws per hit) is the reference's.
-template <int STACK, bool STATS, int MODE>
-__device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfast::Stack<(STACK < 16 ? STACK : 16)>& stk,
-                                                 uint32_t* const scratch) {
-    if (a.gate && *a.gate != a.gate_value) return;  // foreign scenes: the other tracer renders this frame
-    const float4* nodes4 = reinterpret_cast<const float4*>(a.nodes);
-    const float4* tris = reinterpret_cast<const float4*>(a.tris);
-    // this lane's pixel: slot k*256 + tid of the launch's list (k < 0: none)
-    int x = 0, y = 0;
-    bool pixel = false;
-    size_t slot = 0;
-    rt_rng_state* rs = a.rng;
-    rtm::Xorwow rng{0, 0, 0, 0, 0, 0};
-    auto bind = [&](int k, int tid) {
-        const int tile = k >= 0 ? shard_tile(a, k) : -1;
-        int lx, ly;
-        tile_pixel(tid, &lx, &ly);
-        x = (tile % a.tiles_x) * TILE + lx;
-        y = (tile / a.tiles_x) * TILE + ly;
-        pixel = tile >= 0 && x < a.width && y < a.height;
-        slot = (size_t)(k >= 0 ? k : 0) * (TILE * TILE) + tid;
-        rs = a.rng + (a.out_shard ? slot : (size_t)(pixel ? y : 0) * a.width + (pixel ? x : 0));
-        if (pixel) rng = rtm::Xorwow{rs->d, rs->v[0], rs->v[1], rs->v[2], rs->v[3], rs->v[4]};
-    };
-    // entry i of the launch's lane order: the lane map, or slot i (wave i / 64 = 8x8 sub-tile)
-    auto bind_entry = [&](long long i) {
-        const long long s = a.lane_slots ? (long long)a.lane_slots[i] : i;
-        const bool ok = s >= 0 && s < a.slot_count;  // a bad map entry renders nothing
-        bind(ok ? (int)(s >> 8) : -1, (int)(s & 255));
-    };
-    // one 64-lane workgroup per 8x8 sub-tile: tile k = lb / 4, sub-tile lb % 4
-    const int lb = xcd_block(a.tune);
-    bind_entry((long long)lb * WAVE + threadIdx.x);
-    if (a.lane_slots && lb < a.priority_waves) __builtin_amdgcn_s_setprio(3);  // the frame's long waves
-    // Refill (rt_render_params.refill_lanes): the grid holds only as many waves as fit the GPU at
-    // once; entries [grid x 64, entries) form a queue, and a wave whose idle lanes reach
-    // refill_lanes takes that many entries with one atomic (ballot + mbcnt rank the idle lanes), so
-    // lanes stay busy until the queue drains instead of idling once their own pixel is done.
-    // Waves that start less than half full (split waves of a lane plan) are not refilled.
-    constexpr bool REFILL = (MODE & 64) != 0;  // refill is compiled into its own kernel variants only
-    bool drained = !REFILL || a.queue_head == nullptr || __popcll(__ballot(pixel)) < 32;
-    const long long qbase = (long long)gridDim.x * WAVE;
-    Counters c;
-    const rtm::f3 cam_o = ld3(a.cam.origin), cam_h = ld3(a.cam.horizontal), cam_v = ld3(a.cam.vertical),
-                  cam_ll = ld3(a.cam.lower_left_corner);
-    float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f, acc_a = 0.0f;
-    int sample = 0, bounce = 0;
-    bool path = false;
-    rtm::f3 ro = cam_o, rd = cam_o, color = rtm::mk(0, 0, 0), thr = rtm::mk(1, 1, 1);
-    const bool scene_fast = a.scene_fast != 0;
-    const unsigned long long t_start = ((MODE & 8) || a.wave_clock) ? __builtin_amdgcn_s_memtime() : 0;
-
-    for (;;) {
-        if (!drained) {
-            const unsigned long long idle = __ballot(!pixel && !path);
-            const uint32_t ni = (uint32_t)__popcll(idle);
-            if (ni && (ni >= (uint32_t)a.refill_lanes || !__ballot(path))) {
-                const int lead = __ffsll((long long)idle) - 1;
-                unsigned long long base = 0;
-                if ((int)threadIdx.x == lead) base = atomicAdd(a.queue_head, (unsigned long long)ni);
-                base = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(base >> 32), lead) << 32) |
-                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)base, lead);
-                const long long qn = a.entry_count - qbase;
-                if (!pixel && !path) {
-                    const unsigned long long i =
-                        base + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                    if ((long long)i < qn) {
-                        bind_entry(qbase + (long long)i);
-                        acc_r = acc_g = acc_b = acc_a = 0.0f;
-                        sample = 0;
-                    }
-                }
-                if ((long long)(base + ni) >= qn) drained = true;
-            }
-        }
-        if (pixel && !path) {
-            if (sample < a.spp) {
-                // main_raytracing.cu:190: uv = (pixel + vec2(rng(), rng())) / vec2(W, H), u first
-                const float ru = rng.uniform();
-                const float rv = rng.uniform();
-                const float uvx = ((float)x + ru) / (float)a.width;
-                const float uvy = ((float)y + rv) / (float)a.height;
-                ro = cam_o;  // GPUCamera::GetRay (GPUScene.h:13), not normalized
-                rd = rtm::sub(rtm::add(rtm::add(cam_ll, rtm::muls(cam_h, uvx)), rtm::muls(cam_v, uvy)), cam_o);
-                color = rtm::mk(0, 0, 0);
-                thr = rtm::mk(1, 1, 1);
-                bounce = 0;
-                path = true;
-                if (a.bounces == 0) {  // an empty bounce loop: the sample contributes (0,0,0,1)
-                    acc_a += 1.0f;
-                    sample++;
-                    path = false;
-                    continue;
-                }
-            } else {
-                pixel = false;
-                // main_raytracing.cu:195-199
-                const float fs = (float)a.spp;
-                const rtm::f4 res{acc_r / fs, acc_g / fs, acc_b / fs, acc_a / fs};
-                const float lerp = a.frame_index > 0 ? 1.0f / (float)(a.frame_index + 1) : 1.0f;
-                float4 prev;
-                float4* out;
-                if (a.out_shard) {
-                    prev = a.last ? reinterpret_cast<const float4*>(a.last)[slot] : make_float4(0, 0, 0, 0);
-                    out = a.out_shard + slot;
-                } else {
-                    prev = a.last ? *reinterpret_cast<const float4*>(a.last + (size_t)y * a.pitch + (size_t)x * 16)
-                                  : make_float4(0, 0, 0, 0);
-                    out = reinterpret_cast<float4*>(a.surface + (size_t)y * a.pitch + (size_t)x * 16);
-                }
-                const rtm::f4 o = rtm::mix4(rtm::f4{prev.x, prev.y, prev.z, prev.w}, res, lerp);
-                *out = make_float4(o.x, o.y, o.z, 1.0f);
-                rs->d = rng.d;
-                rs->v[0] = rng.v0;
-                rs->v[1] = rng.v1;
-                rs->v[2] = rng.v2;
-                rs->v[3] = rng.v3;
-                rs->v[4] = rng.v4;
-                // per-pixel work for rt_lane_plan: traversal steps + 3 per big leaf + 1 per segment
-                if ((MODE & 8) && a.lane_cost) a.lane_cost[slot] = c.lane_work + (uint32_t)c.seg;
-            }
-        }
-        if (!__ballot(path)) {
-            if (drained) break;
-            continue;  // every lane idle: refill at the top
-        }
-        if (MODE & 8) c.w_iter++;
-        if (STATS) {
-            c.w_seg += (threadIdx.x & 63) == 0;
-            c.l_seg += path;
-        }
-
-        // GetRayHit (main_raytracing.cu:83-109)
-        rtfast::Hit h;
-        h.best = 1e30f, h.kind = 0, h.id = 0, h.bx = h.by = 0.0f;
-        const rtm::f3 nd = rtm::normalize(rd);
-        if (path) {
-            c.seg++;
-            for (int i = 0; i < a.sphere_count; i++) {
-                const GeometrySphere& sp = a.spheres[i];
-                float dist;
-                if (rtd::intersect_sphere(ro, nd, ld3(sp.position), sp.radius * sp.radius, &dist)) {
-                    if (dist >= h.best) continue;
-                    h.best = dist;
-                    h.kind = 1;
-                    h.id = (uint32_t)i;
-                    if (STATS) c.sacc++;
-                }
-            }
-        }
-        const rtfast::Ray R = rtfast::make_ray(ro, rd, nd, scene_fast);
-        rtfast::trace<STATS, MODE>(nodes4, tris, a.pairs, a.tree, a.ltris, a.flat, a.spairs, a.tune, stk, scratch, R, h,
-                                   path, c);
-        if (!path) continue;
-
-        bool end = shade_segment<STATS>(a, h, ro, rd, nd, rng, color, thr, c);
-        if (++bounce >= a.bounces) end = true;
-        if (end) {
-            acc_r += color.x;
-            acc_g += color.y;
-            acc_b += color.z;
-            acc_a += 1.0f;
-            sample++;
-            path = false;
-        }
-    }
-
-    if (a.seg_counter) {
-        unsigned long long v = c.seg;
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if ((threadIdx.x & 63) == 0) atomicAdd(a.seg_counter, v);
-    }
-    // per-wave cost for cost-aware shard plans (rt_render_params.wave_clock; one store per wave)
-    if (a.wave_clock && threadIdx.x == 0) a.wave_clock[lb] = __builtin_amdgcn_s_memtime() - t_start;
-    unsigned long long lane_max = c.l_small;  // the busiest lane's small steps (timing frame)
-    if (MODE & 8)
-        for (int off = 32; off > 0; off >>= 1) {
-            const unsigned long long o = __shfl_xor(lane_max, off);
-            lane_max = o > lane_max ? o : lane_max;
-        }
-    if ((MODE & 8) && a.stats && threadIdx.x == 0) {  // timing frame: per-wave phase clocks
-        atomicAdd(a.stats + RT_STAT_CYCLES_SMALL, c.cy_small);
-        atomicAdd(a.stats + RT_STAT_CYCLES_BIG, c.cy_big);
-        atomicAdd(a.stats + RT_STAT_CYCLES_TOTAL, __builtin_amdgcn_s_memtime() - t_start);
-        atomicAdd(a.stats + RT_STAT_ROUNDS_COOP, c.r_coop);
-        atomicAdd(a.stats + RT_STAT_ROUNDS_SHARED, c.r_shared);
-        atomicAdd(a.stats + RT_STAT_COOP_RAYS, c.coop_rays);
-        // cooperative leaf-tree walk (wave-level): rays, subtree + cluster tests, triangle rounds
-        atomicAdd(a.stats + RT_STAT_TREE_NODES, c.ktest);
-        atomicAdd(a.stats + RT_STAT_TREE_TRI_TESTS, c.ktri);
-        atomicAdd(a.stats + RT_STAT_WAVE_BIG_TRIS, c.w_big);
-        atomicAdd(a.stats + RT_STAT_LANE_BIG_TRIS, c.l_big);
-        atomicAdd(a.stats + RT_STAT_CYCLES_TREE_CLUSTERS, c.cy_tcl);
-        atomicAdd(a.stats + RT_STAT_CYCLES_TREE_CUT, c.cy_tree);
-        atomicAdd(a.stats + RT_STAT_CYCLES_TREE_TRIS, c.cy_ttri);
-        // RT_TUNE bit 11: per-wave clocks (start, end) after the counters, for load-balance analysis
-        if (a.tune & 2048u) {
-            unsigned long long* w = a.stats + RT_STAT_COUNT + 8 * (size_t)blockIdx.x;
-            w[0] = t_start;
-            w[1] = __builtin_amdgcn_s_memtime();
-            w[2] = c.cy_small;
-            w[3] = c.cy_big;
-            w[4] = c.r_coop + c.r_shared;
-            w[5] = c.w_iter;
-            w[6] = c.w_small;
-            w[7] = lane_max;
-        }
-    }
-    if (STATS) {
-        atomicAdd(a.stats + RT_STAT_SEGMENTS, c.seg);
-        atomicAdd(a.stats + RT_STAT_NODES, c.node);
-        atomicAdd(a.stats + RT_STAT_TRI_TESTS, c.tri);
-        atomicAdd(a.stats + RT_STAT_TRI_ACCEPTS, c.tacc);
-        atomicAdd(a.stats + RT_STAT_SPHERE_ACCEPTS, c.sacc);
-        atomicAdd(a.stats + RT_STAT_HITS, c.hit);
-        atomicAdd(a.stats + RT_STAT_MISSES, c.miss);
-        atomicAdd(a.stats + RT_STAT_WAVE_SMALL_ITERS, c.w_small);
-        atomicAdd(a.stats + RT_STAT_LANE_SMALL, c.l_small);
-        atomicAdd(a.stats + RT_STAT_WAVE_BIG_TRIS, c.w_big);
-        atomicAdd(a.stats + RT_STAT_LANE_BIG_TRIS, c.l_big);
-        atomicAdd(a.stats + RT_STAT_CYCLES_TREE_CLUSTERS, c.cy_tcl);
-        atomicAdd(a.stats + RT_STAT_CYCLES_TREE_CUT, c.cy_tree);
-        atomicAdd(a.stats + RT_STAT_CYCLES_TREE_TRIS, c.cy_ttri);
-        atomicAdd(a.stats + RT_STAT_WAVE_SEGMENT_ITERS, c.w_seg);
-        atomicAdd(a.stats + RT_STAT_LANE_SEGMENTS, c.l_seg);
-        atomicAdd(a.stats + RT_STAT_TREE_NODES, c.ktest);
-        atomicAdd(a.stats + RT_STAT_TREE_TRI_TESTS, c.ktri);
-    }
-}
-
-// The production kernel.  The _w5 / _w6 variants ask the compiler for 5 / 6 waves per SIMD
-// (fewer registers, some spilled) -- an occupancy / spill trade-off (RT_TUNE bits 9-10:
-// 0 = _w5, the default; 1 = unconstrained; 2 = _w6).
-template <int STACK, bool STATS, int MODE>
-__global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
-    constexpr int SL = STACK < 16 ? STACK : 16;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
-    __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
-    __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
-    uint32_t ovf[STACK > SL ? STACK - SL : 1];
-    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds + threadIdx.x, ovf}, scratch_lds);
-}
-template <int STACK, bool STATS, int MODE>
-__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(5))) void render_fast_kernel_w5(RenderArgs a) {
-    constexpr int SL = STACK < 16 ? STACK : 16;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
-    __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
-    __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
-    uint32_t ovf[STACK > SL ? STACK - SL : 1];
-    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds + threadIdx.x, ovf}, scratch_lds);
-}
-template <int STACK, bool STATS, int MODE>
-__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(6))) void render_fast_kernel_w6(RenderArgs a) {
-    constexpr int SL = STACK < 16 ? STACK : 16;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
-    __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
-    __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
-    uint32_t ovf[STACK > SL ? STACK - SL : 1];
-    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds + threadIdx.x, ovf}, scratch_lds);
-}
-template <int STACK, bool STATS, int MODE>
-__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(7))) void render_fast_kernel_w7(RenderArgs a) {
-    constexpr int SL = STACK < 16 ? STACK : 16;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
-    __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
-    __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
-    uint32_t ovf[STACK > SL ? STACK - SL : 1];
-    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds + threadIdx.x, ovf}, scratch_lds);
-}
 
 // ---------------------------------------------------------------------------------------
 // init_rng (Random.cu:3-13): state s <- curand_init(seed, pixel(s), 0)
@@ -876,56 +212,30 @@ const uint32_t* device_jump_table() {
     return d;
 }
 
-template <class Tracer, int STACK, bool STATS>
-hipError_t launch(const RenderArgs& args, int waves, hipStream_t stream) {
-    hipLaunchKernelGGL((render_kernel<Tracer, STACK, STATS>), dim3(waves), dim3(WAVE), 0, stream, args);
-    return hipGetLastError();
-}
-
-// Waves of `kernel` the device holds at once (refill launches size their grid to it).
-template <class K>
-int resident_waves(K kernel) {
-    static std::mutex mu;
-    static std::map<std::pair<int, const void*>, int> cache;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    std::lock_guard<std::mutex> lock(mu);
-    const auto key = std::make_pair(dev, (const void*)kernel);
-    auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
-    // waves per SIMD from the kernel's registers and LDS (the occupancy query over-counts here)
-    hipFuncAttributes fa;
-    int cus = 0;
-    if (hipFuncGetAttributes(&fa, (const void*)kernel) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return 0;
-    const int vgpr_waves = fa.numRegs > 0 ? std::min(8, 512 / ((fa.numRegs + 7) / 8 * 8)) : 8;
-    const int lds_waves = fa.sharedSizeBytes > 0 ? (int)(160 * 1024 / fa.sharedSizeBytes) / 4 : 8;
-    return cache[key] = std::max(1, std::min(vgpr_waves, lds_waves)) * 4 * std::max(cus, 1);
-}
-
-template <class K>
-hipError_t launch_grid(K kernel, const RenderArgs& args, int waves, bool refill, hipStream_t stream) {
-    int grid = waves;
-    if (refill && args.queue_head) {  // refill variants: one grid of resident waves, the rest through the queue
-        const int res = resident_waves(kernel);
-        if (res > 0) grid = std::min(waves, res);
-    }
-    hipLaunchKernelGGL(kernel, dim3(grid), dim3(WAVE), 0, stream, args);
-    return hipGetLastError();
-}
-
-template <int STACK, bool STATS, int MODE>
-hipError_t launch_fast_m(const RenderArgs& args, int waves, hipStream_t stream) {
-    // default: 5 waves per SIMD (96 VGPRs, a few cold spills; 4 % faster than the compiler's 126);
-    // rt_render_params.waves_per_simd = 6: 80 VGPRs.  RT_TUNE bits 9-10 (A/B) override: 1 = the
-    // compiler's own choice, 2 = 6, 3 = 7 waves per SIMD.
-    const uint32_t occ = ((args.tune >> 9) & 3u) ? ((args.tune >> 9) & 3u) : (args.waves_per_simd == 6 ? 2u : 0u);
-    constexpr bool refill = (MODE & 64) != 0;  // only these variants drain a refill queue
-    if (!STATS && occ == 0) return launch_grid(render_fast_kernel_w5<STACK, STATS, MODE>, args, waves, refill, stream);
-    if (!STATS && occ == 2) return launch_grid(render_fast_kernel_w6<STACK, STATS, MODE>, args, waves, refill, stream);
-    if (!STATS && occ == 3) return launch_grid(render_fast_kernel_w7<STACK, STATS, MODE>, args, waves, refill, stream);
-    return launch_grid(render_fast_kernel<STACK, STATS, MODE>, args, waves, refill, stream);
+// The render kernel variant of a frame: the traversal stack of the scene's BVH depth (the DFS holds
+// at most depth + 1 entries; 30 entries -- 7.5 KB of LDS per wave -- still fits 5 waves per SIMD and
+// covers the 4-bunny scene's depth 28), then the MODE bits (rt_fast_body.h render_fast_body), then
+// the translation unit that holds that family (rt_render.h).
+hipError_t launch_fast(const RenderArgs& args, int waves, int depth, bool stats, hipStream_t s) {
+    const int stack = (depth >= 0 && depth + 2 <= 30) ? 30 : (depth >= 0 && depth + 2 <= 40) ? 40 : 64;
+    // statistics: the reference's work on scalar records (RT_TUNE bit 7: through the leaf trees);
+    // RT_TUNE bit 8: a timing frame of the production kernel instead (phase clocks, no counts)
+    if (stats && (args.tune & 256u))
+        return launch_fast_timing(stack, args.tree ? 29 : (args.tune & 4096u) ? 9 : 25, args, waves, s);
+    // per-pixel work (rt_render_params.lane_cost): the timing variant of the production kernel
+    if (!stats && args.lane_cost) return launch_fast_timing(stack, args.tree ? 29 : 25, args, waves, s);
+    if (stats) return launch_fast_stats(stack, (args.tree && (args.tune & 128u)) ? 6 : 2, args, waves, s);
+    // MODE bit 4: inner-node and small-leaf steps in separate iterations (rt_fast.h trace); RT_TUNE
+    // bit 12 turns it off (A/B).  Big leaves: packed pairs in the shared-leaf loop, scalar records in
+    // cooperative rounds (MODE 1, measured best); leaf trees compiled in only for scenes that have
+    // them (MODE bit 2); A/B: RT_TUNE bits 4-5 = 2 scalar only, 3 pairs everywhere.
+    const bool split = (args.tune & 4096u) == 0;
+    if (args.queue_head) return launch_fast_refill(stack, args.tree ? 85 : 81, args, waves, s);  // refill: own variants
+    if (args.tree) return split ? launch_fast_prod(stack, 21, args, waves, s) : launch_fast_ab(stack, 5, args, waves, s);
+    const uint32_t mode = (args.tune >> 4) & 3u;
+    if (mode == 2) return launch_fast_ab(stack, 2, args, waves, s);
+    if (mode == 3) return launch_fast_ab(stack, 0, args, waves, s);
+    return split ? launch_fast_prod(stack, 17, args, waves, s) : launch_fast_ab(stack, 1, args, waves, s);
 }
 
 // Per-(device, stream) queue counter of refill launches, zeroed on the stream before each launch.
@@ -938,58 +248,6 @@ unsigned long long* queue_counter(hipStream_t s) {
     auto& c = counters[std::make_pair(dev, s)];
     if (!c && hipMalloc(&c, sizeof(unsigned long long)) != hipSuccess) c = nullptr;
     return c;
-}
-
-template <int STACK, bool STATS>
-hipError_t launch_fast_t(const RenderArgs& args, int waves, hipStream_t stream) {
-
-    // statistics: the reference's work on scalar records (RT_TUNE bit 7: through the leaf trees);
-    // RT_TUNE bit 8: a timing frame of the production kernel instead (phase clocks, no counts)
-    if (STATS && (args.tune & 256u))
-        return args.tree ? launch_fast_m<STACK, false, 29>(args, waves, stream)
-               : (args.tune & 4096u) ? launch_fast_m<STACK, false, 9>(args, waves, stream)
-                                     : launch_fast_m<STACK, false, 25>(args, waves, stream);
-    // per-pixel work (rt_render_params.lane_cost): the timing variant of the production kernel
-    if (!STATS && args.lane_cost)
-        return args.tree ? launch_fast_m<STACK, false, 29>(args, waves, stream) : launch_fast_m<STACK, false, 25>(args, waves, stream);
-    if (STATS) return (args.tree && (args.tune & 128u)) ? launch_fast_m<STACK, STATS, 6>(args, waves, stream)
-                                                        : launch_fast_m<STACK, STATS, 2>(args, waves, stream);
-    // big leaves: packed pairs in the shared-leaf loop, scalar records in cooperative rounds
-    // (MODE 1, measured best), leaf trees compiled in only for scenes that have them (MODE 5);
-    // A/B: RT_TUNE bits 4-5 = 2 scalar only, 3 pairs everywhere
-    // MODE bit 4: inner-node and small-leaf steps in separate iterations (rt_fast.h trace);
-    // RT_TUNE bit 12 turns it off (A/B)
-    const bool split = (args.tune & 4096u) == 0;
-    if (args.queue_head)  // refill (rt_render_params.refill_lanes): its own variants
-        return args.tree ? launch_fast_m<STACK, STATS, 85>(args, waves, stream) : launch_fast_m<STACK, STATS, 81>(args, waves, stream);
-    if (args.tree) return split ? launch_fast_m<STACK, STATS, 21>(args, waves, stream)
-                                : launch_fast_m<STACK, STATS, 5>(args, waves, stream);
-    const uint32_t mode = (args.tune >> 4) & 3u;
-    if (mode == 2) return launch_fast_m<STACK, STATS, 2>(args, waves, stream);
-    if (mode == 3) return launch_fast_m<STACK, STATS, 0>(args, waves, stream);
-    return split ? launch_fast_m<STACK, STATS, 17>(args, waves, stream) : launch_fast_m<STACK, STATS, 1>(args, waves, stream);
-}
-
-hipError_t launch_fast(const RenderArgs& args, int waves, int depth, bool stats, hipStream_t s) {
-    // 30 entries: 7.5 KB of LDS per wave (+256 B scratch in tree scenes) still fits 5 waves per
-    // SIMD, and covers the 4-bunny scene's depth 28 (STACK 40 would leave it at 3 waves per SIMD)
-    if (depth >= 0 && depth + 2 <= 30)
-        return stats ? launch_fast_t<30, true>(args, waves, s) : launch_fast_t<30, false>(args, waves, s);
-    if (depth >= 0 && depth + 2 <= 40)
-        return stats ? launch_fast_t<40, true>(args, waves, s) : launch_fast_t<40, false>(args, waves, s);
-    return stats ? launch_fast_t<64, true>(args, waves, s) : launch_fast_t<64, false>(args, waves, s);
-}
-
-template <class Tracer>
-hipError_t launch_variant(const RenderArgs& args, int waves, int depth, bool stats, hipStream_t s) {
-    // The DFS holds at most depth + 1 entries (one pending sibling per level).  Depth is known
-    // when the scene came through rt_scene_upload; otherwise use the reference's 64
-    // (main_raytracing.cu:35).
-    if (depth >= 0 && depth + 2 <= 28)
-        return stats ? launch<Tracer, 28, true>(args, waves, s) : launch<Tracer, 28, false>(args, waves, s);
-    if (depth >= 0 && depth + 2 <= 40)
-        return stats ? launch<Tracer, 40, true>(args, waves, s) : launch<Tracer, 40, false>(args, waves, s);
-    return stats ? launch<Tracer, 64, true>(args, waves, s) : launch<Tracer, 64, false>(args, waves, s);
 }
 
 int tiles_of_shard(int width, int height, int shard_index, int shard_count) {
@@ -1367,6 +625,8 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     if (p->refill_lanes < 0 || p->refill_lanes > 64) return set_error("rt_render: refill_lanes must be in [0, 64]");
     if (p->waves_per_simd != 0 && p->waves_per_simd != 5 && p->waves_per_simd != 6)
         return set_error("rt_render: waves_per_simd must be 0, 5 or 6");
+    if (((p->tune >> 9) & 3u) == 1u || ((p->tune >> 9) & 3u) == 3u)
+        return set_error("rt_render: RT_TUNE occupancy overrides 1 (compiler's choice) and 3 (7 waves per SIMD) are not built");
     a.waves_per_simd = p->waves_per_simd;
     a.refill_lanes = p->refill_lanes;
     // Every device buffer must cover what the launch touches: a short buffer would fault the GPU.
@@ -1425,16 +685,16 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     hipError_t e;
     if (gate) {  // foreign scene with a mirror: exactly one of the two runs, by the frame's fingerprint
         a.gate = gate, a.gate_value = 1;
-        e = want_flat ? launch_variant<FlatTracer>(a, tiles * 4, depth, stats, s) : launch_fast(a, waves, depth, stats, s);
+        e = want_flat ? launch_ref_tracer(true, a, tiles * 4, depth, stats, s) : launch_fast(a, waves, depth, stats, s);
         if (e == hipSuccess) {
             RenderArgs r = a;
             r.tris = nullptr, r.gate_value = 0;
-            e = launch_variant<RefTracer>(r, tiles * 4, -1, stats, s);
+            e = launch_ref_tracer(false, r, tiles * 4, -1, stats, s);
         }
     } else if (!a.tris)
-        e = launch_variant<RefTracer>(a, tiles * 4, depth, stats, s);
+        e = launch_ref_tracer(false, a, tiles * 4, depth, stats, s);
     else if (want_flat)
-        e = launch_variant<FlatTracer>(a, tiles * 4, depth, stats, s);
+        e = launch_ref_tracer(true, a, tiles * 4, depth, stats, s);
     else
         e = launch_fast(a, waves, depth, stats, s);
     return check(e, "render_kernel launch");

@@ -1,0 +1,21 @@
+// rt_render.h -- launchers of the render kernels, one family per translation unit (rt_kernel.hip
+// dispatches; the families compile in parallel).  `stack` is the traversal stack size of the
+// instantiation (30, 40 or 64 entries: the scene's BVH depth + 2 rounded up), `mode` the MODE bits of
+// render_fast_body (rt_fast_body.h).  Each returns hipErrorInvalidValue for a mode it does not hold.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "rt_common.h"
+
+namespace rtk {
+
+hipError_t launch_fast_prod(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);    // 17, 21
+hipError_t launch_fast_timing(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);  // 25, 29, 9
+hipError_t launch_fast_stats(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);   // 2, 6 (counting)
+hipError_t launch_fast_ab(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);      // 1, 5, 2, 0
+hipError_t launch_fast_refill(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);  // 81, 85
+// The reference-layout tracer (flat = false) or the exact-division flat tracer (rt_ref.hip).
+hipError_t launch_ref_tracer(bool flat, const RenderArgs& a, int waves, int depth, bool stats, hipStream_t s);
+
+}  // namespace rtk

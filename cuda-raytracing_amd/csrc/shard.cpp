@@ -89,7 +89,8 @@ extern "C" int rt_shard_plan(int width, int height, int shard_count, const doubl
 // E = max c x (sum c / max c)^0.34 work units, a lone lane running one unit per unit of time;
 // the whole rank needs about sum c / P units of time when the GPU is full, P = the lanes' worth
 // of work the device does in parallel (MI355X, config 2: 16.4 ms for 634 M units, 2.4 ms for the
-// 3,970-unit pixel alone: P ~ 24,000).  The plan keeps every 8x8 sub-tile wave whose E is within
+// 3,970-unit pixel alone: P ~ 24,000 by this estimate; swept on the device, P = 48,000 gave the
+// fastest shards for configs 2 and 3 at N = 2-8, and bench.py --lane-units ships that).  The plan keeps every 8x8 sub-tile wave whose E is within
 // the target B = slack x max(max c, sum c / P) and splits the others (their pixels in decreasing
 // work, first fit into sub-waves of E <= B: pixels of one sub-tile stay together, so their rays
 // stay coherent).  Waves with E >= B / 2 go first, longest first (the tail starts at t = 0), the

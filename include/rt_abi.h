@@ -171,8 +171,9 @@ typedef struct rt_render_params {
      * the round-robin tile shard_index + k * shard_count.  NULL = round-robin. */
     const int32_t* tile_list;
     int64_t tile_count;
-    /* Optional DEVICE uint64 [entries][4]: elapsed shader-clock ticks of each 8x8 sub-tile wave
-     * of the production tracer (the cost input of rt_shard_plan). */
+    /* Optional DEVICE uint64 [entries][4]: elapsed ticks of the device's constant 100 MHz clock
+     * (s_memrealtime) of each 8x8 sub-tile wave of the production tracer (the cost input of
+     * rt_shard_plan). */
     uint64_t* wave_clock;
     uint32_t tune;                 /* diagnostic A/B knobs (tools/); 0 = the production path */
     /* Optional lane map (production tracer only): wave w, lane l renders slot lane_slots[64w + l]
@@ -182,8 +183,9 @@ typedef struct rt_render_params {
      * costliest pixels (the serial tail of a strong-scaled frame). */
     const int32_t* lane_slots;
     int64_t lane_slot_count;
-    /* Optional DEVICE uint32 [slots]: shader-clock ticks from the start of a slot's wave until
-     * its pixel finished (production tracer; the cost input of rt_lane_plan). */
+    /* Optional DEVICE uint32 [slots]: per-pixel work of the frame, counted deterministically by the
+     * timing variant of the production tracer (its own traversal steps + 3 per big-leaf visit + 1
+     * per segment; no clock involved) -- the cost input of rt_lane_plan. */
     uint32_t* lane_cost;
     /* With a lane map: the first priority_waves waves (rt_lane_plan's long waves) issue at raised
      * wave priority, so the frame's serial tail does not queue behind the short waves. */
@@ -288,7 +290,8 @@ int64_t rt_lane_plan_capacity(int64_t slots);
  * max c x (sum c / max c)^0.34 work units; every 8x8 sub-tile wave above the target
  * slack x max(max c, sum c / parallel_units) is split (first fit, heaviest pixels first) into
  * sub-waves within it.  Waves of at least half the target go first, longest first; the rest keep
- * list order.  parallel_units <= 0: the identity map.  parallel_units ~ 24000 on MI355X (shard.cpp).
+ * list order.  parallel_units <= 0: the identity map.  MI355X: 48000 (bench.py --lane-units; measured
+ * best for configs 2 and 3 at N = 2-8).
  * *long_waves (optional) receives the number of those leading waves (rt_render_params.
  * priority_waves).  Returns the entries written (a multiple of 64), or -1 on bad arguments. */
 int64_t rt_lane_plan(const uint32_t* cost, int64_t slots, double parallel_units, double slack,

@@ -907,6 +907,43 @@ int oracle_render_costs(const OScene* s, int width, int height, int spp, int bou
                        stats, costs);
 }
 
+/*
+ * One camera sample of pixel (x, y) started at every even RNG offset: the reference's sample
+ * body (main_raytracing.cu:188-193: u, v, GetRay, ray_color) run from `state` advanced by
+ * o = 2i draws, i < n.  A sample draws 2 + 4 * (hits) numbers, so o_{j+1} = o_j + draws(o_j)
+ * from o_0 = 0 is the pixel's real sample chain and the table answers "what would sample j
+ * return if it started at o" for every o.  out[8 * i] = color r, g, b, draws consumed,
+ * segments, node visits, triangle tests, 0 (floats; counts exact below 2^24).
+ */
+int oracle_sample_table(const OScene* s, int width, int height, int x, int y, int bounces, const uint32_t state[6],
+                        int n, float* out) {
+    if (!s || width <= 0 || height <= 0 || n < 0) return 1;
+    OCamera cam;
+    o_camera(s, width, height, &cam);
+    float ey = 3.1415926536f * 0.5f, e0 = 0.0f * 0.5f;
+    float cx = o_cos(e0), cy = o_cos(ey), cz = o_cos(e0), sx = o_sin(e0), sy = o_sin(ey), sz = o_sin(e0);
+    float q[4] = {cx * cy * cz + sx * sy * sz, sx * cy * cz - cx * sy * sz, cx * sy * cz + sx * cy * sz, cx * cy * sz - sx * sy * cz};
+    v3 co = V(cam.origin[0], cam.origin[1], cam.origin[2]), ch = V(cam.horizontal[0], cam.horizontal[1], cam.horizontal[2]);
+    v3 cv = V(cam.vertical[0], cam.vertical[1], cam.vertical[2]), cl = V(cam.llc[0], cam.llc[1], cam.llc[2]);
+    ORng base = {state[0], {state[1], state[2], state[3], state[4], state[5]}};
+    for (int i = 0; i < n; i++) {
+        ORng r = base;
+        uint32_t d0 = r.d;
+        OStats st = {0};
+        float ru = rng_uniform(&r), rv = rng_uniform(&r);
+        float ux = ((float)x + ru) / (float)width, uy = ((float)y + rv) / (float)height;
+        v3 rd = vsub(vadd(vadd(cl, vscale(ch, ux)), vscale(cv, uy)), co);
+        v3 c = ray_color(s, co, rd, &r, bounces, q, &st);
+        float* o = out + 8 * (size_t)i;
+        o[0] = c.x; o[1] = c.y; o[2] = c.z;
+        o[3] = (float)((r.d - d0) / 362437u);
+        o[4] = (float)st.seg; o[5] = (float)st.nodes; o[6] = (float)st.tris; o[7] = 0.0f;
+        rng_next(&base);
+        rng_next(&base);
+    }
+    return 0;
+}
+
 /* ------------------------------------------------------------------------------------ */
 /* The glm pieces of the restatement, exported so tests/test_oracle_glm.py can pin them     */
 /* bit for bit against the reference's own vendored glm (oracle/ref_glm.cpp, built from   */

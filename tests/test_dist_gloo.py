@@ -183,19 +183,52 @@ def test_shard_plan_rejects_bad_costs():
 
 
 def test_wave_clock_sanitizer_feeds_a_valid_plan():
-    """bench.py's probe-frame clocks: a wrapped (negative) per-wave delta -- a wave context-switched
-    between two ranks sharing one GPU -- becomes the mean of the valid ones, so rt_shard_plan
-    (which rejects costs < 0) still deals the tiles."""
+    """bench.py's probe-frame clocks (s_memrealtime deltas, one 100 MHz time base): the sanitiser
+    stays as a guard.  A wrapped (negative) delta, one longer than the probe frame's wall time and
+    an inflated positive outlier (> 4096x the median) all become the median of the others, so
+    rt_shard_plan (which rejects costs < 0) still deals the tiles and no outlier skews it."""
     import bench
 
     rt = T.load_rt()
     tiles = rt.sharding.tiles_total(64, 64)
     clocks = np.arange(1, 4 * tiles + 1, dtype=np.int64) * 1000
-    clocks[5] = -(1 << 40)
-    c, nbad = bench.sanitize_wave_clocks(clocks)
-    assert nbad == 1 and (c >= 0).all()
-    assert c[5] == np.delete(clocks, 5).astype(np.float64).mean()
-    ok, n0 = bench.sanitize_wave_clocks(clocks[6:])
-    assert n0 == 0 and np.array_equal(ok, clocks[6:].astype(np.float64))
+    clocks[5] = -(1 << 40)      # wrapped
+    clocks[9] = 1 << 40         # beyond the probe's wall time
+    clocks[11] = 1000 * 4 * tiles * 10000  # inflated: > 4096x the median, still inside the wall time
+    wall_s = float(clocks[11]) / bench.CLOCK_HZ * 2
+    c, nbad = bench.sanitize_wave_clocks(clocks, wall_s=wall_s)
+    assert nbad == 3 and (c >= 0).all()
+    med = np.median(np.delete(clocks, [5, 9, 11]).astype(np.float64))
+    assert c[5] == c[9] == c[11] == med
+    ok, n0 = bench.sanitize_wave_clocks(clocks[12:], wall_s=wall_s)
+    assert n0 == 0 and np.array_equal(ok, clocks[12:].astype(np.float64))
     lists, counts = rt.shard_plan(64, 64, 2, c.reshape(-1, 4).sum(1))
     assert sorted(np.concatenate([lists[r, : counts[r]] for r in range(2)]).tolist()) == list(range(tiles))
+
+
+def test_launcher_deadline_kills_stalled_job():
+    """bench.launch_ranks: a job whose rank 1 stalls before a collective is killed whole at the
+    deadline and the launcher returns 124 (instead of holding the driver until its own timeout)."""
+    import subprocess
+    import sys
+    import time
+
+    import bench
+
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "helpers", "stall_rank.py")
+    t0 = time.monotonic()
+    rc = bench.launch_ranks(2, cmd=[sys.executable, script], deadline_s=20.0)
+    assert rc == 124 and time.monotonic() - t0 < 60
+    # the per-rank watchdog (launches under torch.distributed.run): rank 1 ends itself with 124,
+    # rank 0 then fails its collective or reaches its own deadline
+    env = dict(os.environ, STALL_DEADLINE="15")
+    t0 = time.monotonic()
+    procs = []
+    port = str(_free_port())
+    for r in range(2):
+        e = dict(env, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, script], env=e, stderr=subprocess.PIPE, text=True))
+    out = [p.communicate(timeout=90)[1] for p in procs]
+    assert procs[1].returncode == 124 and "deadline exceeded in phase 'collective'" in out[1]
+    assert procs[0].returncode != 0
+    assert time.monotonic() - t0 < 90

@@ -127,3 +127,76 @@ def test_config4_full_frame_vs_reference_layout_tracer(rt):
     ref, rrng = render_gpu(rt, "bunny4", w, h, 8, 6, tracer="ref")
     report("config4 full frame: production vs reference-layout tracer", fast, ref)
     assert np.array_equal(frng, rrng)
+
+
+def test_config3_sharded_8way_equals_unsharded(rt):
+    """BASELINE configs[2] (3840x2160, 64 spp) through the multi-GPU data path at full size, the 8
+    ranks rendered one after the other on this device exactly as bench.py --gpus 8 runs them:
+    probe frame with per-wave clocks on each rank's round-robin tiles -> rt_shard_plan (longest
+    processing time first) -> per rank rt_init_rng_tiles, a lane-cost probe on a copy of its RNG
+    states, rt_lane_plan (parallel_units 48000), the shard rendered through its lane map ->
+    rt_unshard_tiles.  The reassembled frame and every pixel's final RNG state equal the unsharded
+    production frame bit for bit; the unsharded frame in turn equals the reference-layout tracer
+    (the reference's own loop, main_raytracing.cu:33-200) over the whole frame.  The oracle pins
+    8 bands of it in test_row_bands_vs_oracle."""
+    import bench
+
+    w, h, spp, b, n = 3840, 2160, 64, 6, 8
+    full, rng_full = render_gpu(rt, "bunny", w, h, spp, b)
+    s = rt.Scene()
+    s.setup("bunny")
+    s.set_viewport(w, h)
+    # probe (bench.make_plan): each rank's round-robin tiles once, per-wave clocks
+    rr, rc = rt.shard_plan(w, h, n)
+    cost = np.zeros(rt.sharding.tiles_total(w, h))
+    for r in range(n):
+        mine = torch.from_numpy(rr[r, : rc[r]]).cuda()
+        rng = rt.alloc_rng(int(rc[r]) * 256)
+        rt.init_rng_tiles(rng, w, h, mine, T.SEED)
+        s.upload(rng.data_ptr())
+        out = torch.zeros((int(rc[r]) * 256, 4), dtype=torch.float32, device="cuda")
+        clk = torch.zeros(int(rc[r]) * 4, dtype=torch.int64, device="cuda")
+        rt.render(s, None, None, w, h, spp, b, 0, r, n, out_shard=out, tile_list=mine, wave_clock=clk)
+        torch.cuda.synchronize()
+        c, nbad = bench.sanitize_wave_clocks(clk.cpu().numpy())
+        assert nbad == 0, "one process: every probe clock is valid"
+        cost[rr[r, : rc[r]]] = c.reshape(-1, 4).sum(1)
+        del rng, out, clk
+    lists, counts = rt.shard_plan(w, h, n, cost)
+    cap = lists.shape[1]
+    shards = torch.zeros((n, cap * 256, 4), dtype=torch.float32, device="cuda")
+    rng_ok = True
+    waves = []
+    for r in range(n):
+        mine = torch.from_numpy(lists[r, : counts[r]]).cuda()
+        rng = rt.alloc_rng(cap * 256)
+        rt.init_rng_tiles(rng, w, h, mine, T.SEED)
+        s.upload(rng.data_ptr())
+        saved = rng.clone()
+        pc = torch.zeros(int(counts[r]) * 256, dtype=torch.int32, device="cuda")
+        rt.render(s, None, None, w, h, spp, b, 0, r, n, out_shard=shards[r], tile_list=mine, lane_cost=pc)
+        torch.cuda.synchronize()
+        rng.copy_(saved)
+        m, nlong = rt.lane_plan(pc.cpu().numpy(), 48000.0, 1.0)
+        waves.append(int(m.size // 64))
+        shards[r].zero_()
+        rt.render(s, None, None, w, h, spp, b, 0, r, n, out_shard=shards[r], tile_list=mine,
+                  lane_slots=torch.from_numpy(m).cuda(), priority_waves=nlong)
+        torch.cuda.synchronize()
+        # final RNG states of the shard's pixels == the unsharded frame's states of those pixels
+        xs, ys = rt.sharding.slot_pixels(w, h, r, n, int(counts[r]), lists[r, : counts[r]])
+        ok = xs >= 0
+        got_rng = rng.view(-1, 12)[: int(counts[r]) * 256, :6].cpu().numpy().view(np.uint32)[ok]
+        rng_ok &= bool(np.array_equal(got_rng, rng_full[(ys[ok] * w + xs[ok]).astype(np.int64)]))
+        del rng, saved, pc
+    frame = rt.alloc_surface(w, h)
+    rt.unshard_tiles(frame, w, h, shards, torch.from_numpy(lists).cuda())
+    torch.cuda.synchronize()
+    got = rt.surface_view(frame, w).cpu().numpy()
+    report("config3 8-way LPT + lane-plan shards reassembled vs unsharded, 3840x2160 64spp", got, full,
+           {"ranks": n, "tiles_per_rank": [int(c) for c in counts], "lane_plan_waves": waves})
+    assert rng_ok, "config 3: final RNG states of the sharded render differ"
+    del got, frame, shards
+    ref, rng_ref = render_gpu(rt, "bunny", w, h, spp, b, tracer="ref")
+    report("config3 full frame: production vs reference-layout tracer, 3840x2160 64spp", full, ref)
+    assert np.array_equal(rng_full, rng_ref)

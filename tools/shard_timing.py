@@ -67,7 +67,7 @@ def lane_map(rt, scene, W, H, SPP, BOUNCES, mine, rng, lane):
         top = np.argsort(-wc)[:5]
         print(json.dumps({"slots": int(c.size), "cmax": int(c.max()), "csum": int(c.sum()), "R": round(float(c.sum()) / c.max(), 1),
                           "p99": float(np.percentile(c[c > 0], 99)), "waves": int(len(mw)), "long": nlong, "first_full_wave": nh,
-                          "top_waves": [[int(i), round(float(wc[i]) / 2.4e6, 2), int((mw[i] >= 0).sum()),
+                          "top_waves": [[int(i), round(float(wc[i]) / 1e5, 3), int((mw[i] >= 0).sum()),
                                          int(c[mw[i][mw[i] >= 0]].max()), int(c[mw[i][mw[i] >= 0]].sum())] for i in top]}),
               flush=True)
     return lm, nlong

@@ -48,6 +48,7 @@ __global__ __launch_bounds__(64) void bench(float* out, unsigned long long* clk,
           a7 = a0 + 7, b = seed * 0.5f;
     f2 p0 = {a0, a1}, p1 = {a1, a2}, p2 = {a2, a3}, p3 = {a3, a4}, p4 = {a4, a5}, p5 = {a5, a6}, p6 = {a6, a7},
        p7 = {a7, a0}, q = {b, b};
+    uint32_t sreg = (uint32_t)__builtin_amdgcn_readfirstlane((int)blockIdx.x);
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     for (int i = 0; i < ITERS; i++) {
 #pragma unroll
@@ -68,11 +69,21 @@ __global__ __launch_bounds__(64) void bench(float* out, unsigned long long* clk,
             if constexpr (K == 13) { OP8("v_cmp_lt_f32 vcc, %0, %1") }
             if constexpr (K == 14) { OP8("v_lshlrev_b32 %0, 2, %0") }
             if constexpr (K == 15) { OP8("v_mov_b32 %0, %1") }
+            if constexpr (K == 16) {  // one VALU + one independent SALU per slot (do they co-issue?)
+                asm volatile("v_add_f32 %0, %0, %2\n s_add_u32 %1, %1, 1" : "+v"(a0), "+s"(sreg) : "v"(b) : "scc");
+                asm volatile("v_add_f32 %0, %0, %2\n s_add_u32 %1, %1, 1" : "+v"(a1), "+s"(sreg) : "v"(b) : "scc");
+                asm volatile("v_add_f32 %0, %0, %2\n s_add_u32 %1, %1, 1" : "+v"(a2), "+s"(sreg) : "v"(b) : "scc");
+                asm volatile("v_add_f32 %0, %0, %2\n s_add_u32 %1, %1, 1" : "+v"(a3), "+s"(sreg) : "v"(b) : "scc");
+                asm volatile("v_add_f32 %0, %0, %2\n s_add_u32 %1, %1, 1" : "+v"(a4), "+s"(sreg) : "v"(b) : "scc");
+                asm volatile("v_add_f32 %0, %0, %2\n s_add_u32 %1, %1, 1" : "+v"(a5), "+s"(sreg) : "v"(b) : "scc");
+                asm volatile("v_add_f32 %0, %0, %2\n s_add_u32 %1, %1, 1" : "+v"(a6), "+s"(sreg) : "v"(b) : "scc");
+                asm volatile("v_add_f32 %0, %0, %2\n s_add_u32 %1, %1, 1" : "+v"(a7), "+s"(sreg) : "v"(b) : "scc");
+            }
         }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     const f2 ps = p0 + p1 + p2 + p3 + p4 + p5 + p6 + p7;
-    out[blockIdx.x * 64 + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + ps.x + ps.y;
+    out[blockIdx.x * 64 + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + ps.x + ps.y + (float)sreg;
     if (threadIdx.x == 0) {
         clk[2 * blockIdx.x] = t1 - t0;
         clk[2 * blockIdx.x + 1] = r1 - r0;
@@ -103,7 +114,7 @@ int run(const char* name, int waves_per_simd, int cus) {
     for (int i = 0; i < blocks; i++) cyc += c[2 * i], real += c[2 * i + 1];
     cyc /= blocks, real /= blocks;
     const double ghz = cyc / (real / 100e6) / 1e9;  // s_memrealtime ticks at 100 MHz
-    const int per_op = (K == 6) ? 2 : 1;
+    const int per_op = (K == 6) ? 2 : 1;  // K == 16 counts the VALU instructions only
     const double instr_per_wave = (double)ITERS * UNROLL * 8 * per_op;
     // per SIMD: waves_per_simd waves, each instr_per_wave instructions, in `cyc` cycles
     std::printf("%-24s waves/SIMD %d  %.2f cycles per wave-instruction per SIMD (wave clock %.3g cyc, %.2f GHz, %.3f ms)\n",
@@ -116,7 +127,8 @@ int run(const char* name, int waves_per_simd, int cus) {
 int main() {
     int cus = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
-    for (int w : {1, 4, 8}) {
+    for (int w : {1, 2, 3, 4, 6, 8}) {
+        run<16>("v_add_f32 + s_add_u32", w, cus);
         run<0>("v_add_f32", w, cus);
         run<1>("v_fma_f32", w, cus);
         run<10>("v_mul_f32", w, cus);
