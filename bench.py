@@ -368,6 +368,14 @@ def sanitize_wave_clocks(clocks, wall_s=None, k=4096.0):
     return c, int(bad.sum())
 
 
+def gather_layout(counts, cap):
+    """The frame gather's bookkeeping (rt_gather_shards): rank r sends its first counts[r] tiles of
+    256 float4 slots (recv_bytes[r] bytes); the root lays rank r's bytes at r * stride, stride = the
+    plan capacity's worth of tiles.  Slots past counts[r] * 256 in row r are padding that
+    rt_unshard_tiles never reads (their tile-list entries are -1)."""
+    return [int(c) * 256 * 16 for c in counts], int(cap) * 256 * 16
+
+
 def make_plan(rt, scene, W, H, SPP, BOUNCES, rank, world, plan_kind, dev):
     """(tile_lists [world, cap] int32 numpy, counts, probe info).  'cost': every rank renders its
     round-robin tiles once with per-wave clocks (set-up, untimed, throw-away RNG), the per-tile
@@ -577,7 +585,7 @@ def run(args):
             gather_kind = "rt_gather_shards (RCCL send/recv group, librt_hip.so)"
         else:
             gather_kind = f"torch.distributed.gather ({args.backend})"
-    recv_bytes = [int(c) * 256 * 16 for c in counts] if sharded else None
+    recv_bytes = gather_layout(counts, lists.shape[1])[0] if sharded else None
 
     seg_counter = torch.zeros(1, dtype=torch.int64, device=dev)
     n_total = args.warmup + args.steps

@@ -74,7 +74,7 @@ class RenderParams(ctypes.Structure):
                 ("tile_list", ctypes.c_void_p), ("tile_count", ctypes.c_int64), ("wave_clock", ctypes.c_void_p),
                 ("tune", ctypes.c_uint32), ("lane_slots", ctypes.c_void_p), ("lane_slot_count", ctypes.c_int64),
                 ("lane_cost", ctypes.c_void_p), ("priority_waves", ctypes.c_int64), ("refill_lanes", ctypes.c_int32),
-                ("waves_per_simd", ctypes.c_int32)]
+                ("waves_per_simd", ctypes.c_int32), ("lone_slots", ctypes.c_void_p), ("lone_count", ctypes.c_int64)]
 
 
 assert ctypes.sizeof(GPUScene) == 136 and ctypes.sizeof(GPUMaterial) == 64
@@ -97,6 +97,7 @@ SIGNATURES = {
     "rt_set_build_options": (_I, [_P]),
     "rt_lane_plan_capacity": (ctypes.c_int64, [ctypes.c_int64]),
     "rt_lane_plan": (ctypes.c_int64, [_P, ctypes.c_int64, ctypes.c_double, ctypes.c_double, _P, ctypes.c_int64, _P]),
+    "rt_lone_plan": (ctypes.c_int64, [_P, ctypes.c_int64, ctypes.c_int64, _U32, _P]),
     "rt_init_rng_tiles": (_I, [_P, _I, _I, _P, ctypes.c_int64, _U32, _P]),
     "rt_unshard_tiles": (_I, [_P, _U64, _I, _I, _I, _P, ctypes.c_int64, _P, _P]),
     "rt_comm_unique_id": (_I, [_P]),
@@ -342,13 +343,17 @@ def init_rng_states(rng, width, height, seed, shard_index=0, shard_count=1, stre
 def render(scene, surface, last, width, height, spp, bounces, frame_index=0, shard_index=0, shard_count=1,
            out_shard=None, stats=None, segment_counter=None, stream=None, tracer="fast", tile_list=None,
            wave_clock=None, tune=0, lane_slots=None, lane_cost=None, priority_waves=0, refill_lanes=0,
-           waves_per_simd=0):
+           waves_per_simd=0, lone_slots=None):
     """rt_render: one frame (or one shard of it) on `stream` (default: torch's current stream).
     tile_list: device int32 tensor of tile ids (a row of a sharding.Plan) instead of the
     round-robin deal; wave_clock: device int64 tensor [entries*4] receiving per-wave clocks;
     tune: diagnostic A/B knobs (0 = production); lane_slots: device int32 lane map (rt_lane_plan,
-    a multiple of 64 entries); lane_cost: device int32/uint32 [slots] receiving per-pixel clocks."""
+    a multiple of 64 entries); lane_cost: device int32/uint32 [slots] receiving per-pixel work;
+    lone_slots: device int32 slots for the lone-pixel kernel (rt_lone_plan; needs lane_slots)."""
     p = RenderParams()
+    if lone_slots is not None and lone_slots.numel() > 0:
+        assert lone_slots.dtype == torch.int32 and lone_slots.is_cuda and lone_slots.dim() == 1
+        p.lone_slots, p.lone_count = lone_slots.data_ptr(), lone_slots.numel()
     if lane_slots is not None:
         assert lane_slots.dtype == torch.int32 and lane_slots.is_cuda and lane_slots.numel() % 64 == 0
         p.lane_slots, p.lane_slot_count = lane_slots.data_ptr(), lane_slots.numel()
@@ -458,6 +463,17 @@ def lane_plan(cost, parallel_units=48000.0, slack=1.0):
     if n < 0:
         raise RTError("rt_lane_plan failed: " + lib().rt_last_error().decode(errors="replace"))
     return out[:n].copy(), int(nlong.value)
+
+
+def lone_plan(cost, max_lone, min_cost=1):
+    """rt_lone_plan: (int32 numpy lone slots, heaviest first; the cost array with those slots marked
+    for rt_lane_plan) from per-slot work (a probe frame's lane_cost)."""
+    cost = np.ascontiguousarray(np.asarray(cost).astype(np.uint32)).copy()
+    out = np.empty(max(int(max_lone), 1), dtype=np.int32)
+    n = int(lib().rt_lone_plan(cost.ctypes.data, cost.size, int(max_lone), int(min_cost), out.ctypes.data))
+    if n < 0:
+        raise RTError("rt_lone_plan failed: " + lib().rt_last_error().decode(errors="replace"))
+    return out[:n].copy(), cost
 
 
 def init_rng_tiles(rng, width, height, tile_list, seed, stream=None):

@@ -116,6 +116,9 @@ extern "C" int rt_gather_shards(rt_comm* comm, const void* shard, size_t shard_b
             const size_t n = recv_bytes ? recv_bytes[r] : shard_bytes;
             if (n > stride) return nccl_fail("rt_gather_shards: a shard exceeds the stride", ncclInvalidArgument);
         }
+        // the root copies its own recv_bytes[root] bytes out of `shard`: never more than it holds
+        if (recv_bytes && recv_bytes[root] > shard_bytes)
+            return nccl_fail("rt_gather_shards: recv_bytes[root] exceeds the root's shard_bytes", ncclInvalidArgument);
     }
     ncclResult_t r = ncclGroupStart();
     if (r != ncclSuccess) return nccl_fail("ncclGroupStart", r);

@@ -3,6 +3,7 @@
 #include "mirror.h"
 
 #include <cstdlib>
+#include <functional>
 
 #include "leaftree.h"
 
@@ -118,6 +119,75 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
             out->pairs.insert(out->pairs.end(), q, q + 20);
         }
     }
+    rt_build_treelets(nodes, node_count, out->treelets);
+}
+
+// ---------------------------------------------------------------------------------------
+// Treelets (mirror.h, rt_lone.hip).  From treelet root r, nodes are taken breadth first while two
+// more fit into 63 slots; an inner node whose children were not taken is a frontier and roots
+// its own treelet.  Within a treelet the nodes are stored in right-first preorder (first + 1
+// before first, the reference's pop order), so a slot's subtree is the run of slots after it.
+// ---------------------------------------------------------------------------------------
+void rt_build_treelets(const GPUBVHNode* nodes, size_t node_count, std::vector<float>& out) {
+    out.clear();
+    if (node_count == 0 || nodes[0].prim_count > 0) return;  // a leaf root: nothing to walk
+    constexpr uint32_t EMPTY = 0xffffffffu;
+    const float inf = INFINITY;
+    std::vector<uint32_t> roots{0u};
+    for (size_t k = 0; k < roots.size(); k++) {
+        // breadth-first selection
+        std::vector<uint32_t> taken{roots[k]};
+        std::map<uint32_t, bool> expanded;
+        for (size_t q = 0; q < taken.size(); q++) {
+            const GPUBVHNode& nd = nodes[taken[q]];
+            if (nd.prim_count > 0) continue;
+            if (taken.size() + 2 > 63) break;
+            expanded[taken[q]] = true;
+            taken.push_back(nd.first_index + 1);
+            taken.push_back(nd.first_index);
+        }
+        // right-first preorder over the taken subtree: slot, parent slot, subtree size
+        struct Slot { uint32_t node; int parent; uint32_t size; unsigned long long anc; };
+        std::vector<Slot> slots;
+        std::function<uint32_t(uint32_t, int, unsigned long long)> place = [&](uint32_t n, int parent,
+                                                                                unsigned long long anc) -> uint32_t {
+            const uint32_t me = (uint32_t)slots.size();
+            slots.push_back({n, parent, 1u, anc});
+            if (expanded.count(n)) {
+                const unsigned long long a2 = anc | (1ull << me);
+                const uint32_t s1 = place(nodes[n].first_index + 1, (int)me, a2);
+                const uint32_t s2 = place(nodes[n].first_index, (int)me, a2);
+                slots[me].size = 1u + s1 + s2;
+            }
+            return slots[me].size;
+        };
+        place(roots[k], -1, 0ull);
+        const size_t base = out.size();
+        out.resize(base + 64 * 12, 0.0f);
+        for (uint32_t p = 0; p < 64; p++) {
+            float* o = &out[base + p * 12];
+            if (p >= slots.size()) {
+                o[0] = o[1] = o[2] = inf, o[3] = o[4] = o[5] = -inf;
+                std::memcpy(&o[7], &EMPTY, 4);
+                continue;
+            }
+            const GPUBVHNode& nd = nodes[slots[p].node];
+            o[0] = nd.bmin[0], o[1] = nd.bmin[1], o[2] = nd.bmin[2], o[3] = nd.bmax[0], o[4] = nd.bmax[1], o[5] = nd.bmax[2];
+            uint32_t X = nd.first_index, cnt = nd.prim_count, frontier = 0u;
+            if (cnt == 0 && !expanded.count(slots[p].node)) {
+                X = (uint32_t)roots.size();
+                roots.push_back(slots[p].node);
+                frontier = 1u;
+            }
+            std::memcpy(&o[6], &X, 4);
+            std::memcpy(&o[7], &cnt, 4);
+            const uint32_t lo = (uint32_t)slots[p].anc, hi = (uint32_t)(slots[p].anc >> 32);
+            std::memcpy(&o[8], &lo, 4);
+            std::memcpy(&o[9], &hi, 4);
+            std::memcpy(&o[10], &slots[p].size, 4);
+            std::memcpy(&o[11], &frontier, 4);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -142,15 +212,17 @@ void release(Entry& e) {
 
 int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owned, uint64_t fingerprint) {
     const size_t nt = m.tris.size() * 4, np = m.pairs.size() * 4, nk = m.tree.size() * 4, nl = m.ltris.size() * 4,
-                 ns = m.spairs.size() * 4, nf = m.flat.size() * 4;
+                 ns = m.spairs.size() * 4, nf = m.flat.size() * 4, nq = m.treelets.size() * 4;
     void* block = nullptr;
-    if (rt_malloc(&block, nt + np + nk + nl + ns + nf + 64) != 0) return -1;
+    if (rt_malloc(&block, nt + np + nk + nl + ns + nf + nq + 64) != 0) return -1;
     char* b = static_cast<char*>(block);
+    const size_t oq = nt + np + nk + nl + ns + nf;
     if ((nt && rt_memcpy_h2d(b, m.tris.data(), nt) != 0) || (np && rt_memcpy_h2d(b + nt, m.pairs.data(), np) != 0) ||
         (nk && rt_memcpy_h2d(b + nt + np, m.tree.data(), nk) != 0) ||
         (nl && rt_memcpy_h2d(b + nt + np + nk, m.ltris.data(), nl) != 0) ||
         (ns && rt_memcpy_h2d(b + nt + np + nk + nl, m.spairs.data(), ns) != 0) ||
-        (nf && rt_memcpy_h2d(b + nt + np + nk + nl + ns, m.flat.data(), nf) != 0)) {
+        (nf && rt_memcpy_h2d(b + nt + np + nk + nl + ns, m.flat.data(), nf) != 0) ||
+        (nq && rt_memcpy_h2d(b + oq, m.treelets.data(), nq) != 0)) {
         rt_free(block);
         return -1;
     }
@@ -161,6 +233,7 @@ int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owne
     e.dev.ltris = nl ? b + nt + np + nk : nullptr;
     e.dev.spairs = ns ? b + nt + np + nk + nl : nullptr;
     e.dev.flat = nf ? b + nt + np + nk + nl + ns : nullptr;
+    e.dev.treelets = nq ? b + oq : nullptr;
     e.dev.depth = m.depth;
     e.dev.fast = m.fast;
     e.dev.owned = owned;

@@ -19,6 +19,13 @@
 //  * tree / ltris  for leaves of at least MIRROR_TREE_LEAF triangles, a leaf tree instead
 //           (leaftree.h): the first record holds po = the root node, pf = 2;
 //  * flat   the leaf trees' flat cluster and cut lists (leaftree.h, cooperative walk);
+//  * treelets  the BVH cut into subtrees of at most 63 nodes for the lone-pixel kernel
+//           (rt_lone.hip): from a root, nodes are taken breadth first while they fit; the nodes of
+//           a treelet sit in 64 slots of 48 B in right-first preorder (the reference's DFS order,
+//           main_raytracing.cu:75-76): (bmin.xyz, bmax.x), (bmax.yz, X, count), (ancestor-slot
+//           mask lo, hi, subtree size in slots, frontier) -- X = the leaf's first triangle, or for
+//           a frontier (an inner node whose children were not taken) the treelet rooted at it,
+//           which holds the same node again in its slot 0; unused slots have count = ~0u;
 //  * depth  the deepest leaf (sizes the traversal stack) and whether every node bound lies in
 //           the range where the filtered slab test is proven (rt_fast.h).
 #pragma once
@@ -39,6 +46,7 @@ struct MirrorHost {
     std::vector<float> tree;      // 16 floats per leaf-tree node
     std::vector<float> ltris;     // 12 floats per leaf-tree triangle record
     std::vector<float> flat;      // 16 floats per record: leaf trees' flat cluster / cut lists
+    std::vector<float> treelets;  // 64 slots x 12 floats per treelet (rt_lone.hip)
     int depth = 0;                // deepest leaf (root = 0) reachable from node 0
     bool fast = true;             // node bounds inside the filtered-slab range (rt_fast.h)
 };
@@ -49,6 +57,9 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
                      const GPUFace* faces, size_t face_count, const GPUVertex* vertices, size_t vertex_count,
                      MirrorHost* out);
 
+// The treelets alone (also called by rt_build_mirror).
+void rt_build_treelets(const GPUBVHNode* nodes, size_t node_count, std::vector<float>& out);
+
 // Registry: device copies of a mirror, keyed by the GPUScene's BVH node pointer and valid
 // while the scene's face_indices / faces / vertices pointers are the ones it was built from.
 struct MirrorDevice {
@@ -58,6 +69,7 @@ struct MirrorDevice {
     const void* tree = nullptr;
     const void* ltris = nullptr;
     const void* flat = nullptr;
+    const void* treelets = nullptr;
     int depth = -1;
     bool fast = false;
     bool owned = true;         // built by rt_scene_upload, which forgets it before freeing the arrays

@@ -238,6 +238,27 @@ hipError_t launch_fast(const RenderArgs& args, int waves, int depth, bool stats,
     return split ? launch_fast_prod(stack, 17, args, waves, s) : launch_fast_ab(stack, 1, args, waves, s);
 }
 
+// Per-(device, stream) side stream of the lone-pixel kernel and its fork / join events.
+struct LoneStreams {
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+LoneStreams* lone_streams(hipStream_t s) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, LoneStreams> all;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lock(mu);
+    LoneStreams& l = all[std::make_pair(dev, s)];
+    if (!l.side && (hipStreamCreateWithFlags(&l.side, hipStreamNonBlocking) != hipSuccess ||
+                    hipEventCreateWithFlags(&l.fork, hipEventDisableTiming) != hipSuccess ||
+                    hipEventCreateWithFlags(&l.join, hipEventDisableTiming) != hipSuccess)) {
+        l = LoneStreams{};
+        return nullptr;
+    }
+    return &l;
+}
+
 // Per-(device, stream) queue counter of refill launches, zeroed on the stream before each launch.
 unsigned long long* queue_counter(hipStream_t s) {
     static std::mutex mu;
@@ -393,7 +414,7 @@ void upload_mirror(ForeignBuild* b) {
         MirrorHost mh;
         rt_build_mirror(nodes, b->bytes[0] / sizeof(GPUBVHNode), fi, b->bytes[1] / 4, faces, b->bytes[2] / sizeof(GPUFace),
                         verts, b->bytes[3] / sizeof(GPUVertex), &mh);
-        const std::vector<float>* parts[6] = {&mh.tris, &mh.pairs, &mh.tree, &mh.ltris, &mh.spairs, &mh.flat};
+        const std::vector<float>* parts[7] = {&mh.tris, &mh.pairs, &mh.tree, &mh.ltris, &mh.spairs, &mh.flat, &mh.treelets};
         size_t total = 64;
         for (auto* v : parts) total += v->size() * 4;
         hipStream_t st;
@@ -401,8 +422,8 @@ void upload_mirror(ForeignBuild* b) {
         void* block = nullptr;
         if (hipMallocAsync(&block, total, st) != hipSuccess) throw std::runtime_error("mirror allocation failed");
         char* p = static_cast<char*>(block);
-        const void* where[6];
-        for (int i = 0; i < 6; i++) {
+        const void* where[7];
+        for (int i = 0; i < 7; i++) {
             const size_t nb = parts[i]->size() * 4;
             where[i] = nb ? p : nullptr;
             if (nb && hipMemcpyAsync(p, parts[i]->data(), nb, hipMemcpyHostToDevice, st) != hipSuccess)
@@ -414,7 +435,7 @@ void upload_mirror(ForeignBuild* b) {
         if (e != hipSuccess) throw std::runtime_error("mirror upload failed");
         b->block = block;
         b->dev.tris = where[0], b->dev.pairs = where[1], b->dev.tree = where[2], b->dev.ltris = where[3];
-        b->dev.spairs = where[4], b->dev.flat = where[5];
+        b->dev.spairs = where[4], b->dev.flat = where[5], b->dev.treelets = where[6];
         b->dev.depth = mh.depth, b->dev.fast = mh.fast, b->dev.owned = false, b->dev.fingerprint = b->fingerprint;
         b->state = 2;
     } catch (const std::exception& e) {
@@ -676,6 +697,15 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     if ((p->lane_slots || p->lane_cost || p->refill_lanes) && (gate || !a.tris || want_flat))
         return set_error("rt_render: lane_slots / lane_cost / refill_lanes need the production tracer on an rt_scene_upload scene");
     if (p->lane_cost && p->refill_lanes) return set_error("rt_render: lane_cost probes run without refill");
+    const bool lone = p->lone_count > 0;
+    if (p->lone_count < 0 || p->lone_count > (int64_t)1 << 28 || (lone && !p->lone_slots))
+        return set_error("rt_render: lone_count must be in [0, 2^28] with lone_slots");
+    if (lone && (!p->lane_slots || gate || !a.tris || want_flat || stats || p->lane_cost || p->refill_lanes))
+        return set_error("rt_render: lone_slots need lane_slots and the production tracer on an rt_scene_upload scene "
+                         "(no statistics / lane_cost / refill frames)");
+    if (lone && (!mir.treelets || depth < 0 || depth > 75))
+        return set_error("rt_render: lone_slots need the scene's treelets (a BVH of depth <= 75 with an inner root)");
+    if (lone && bytes_from(p->lone_slots) < (size_t)p->lone_count * 4) return set_error("rt_render: lone_slots too small");
     if (p->refill_lanes) {  // the queue counter, zeroed on the launch stream
         a.queue_head = queue_counter(s);
         if (!a.queue_head) return set_error("rt_render: cannot allocate the refill queue counter");
@@ -695,7 +725,17 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
         e = launch_ref_tracer(false, a, tiles * 4, depth, stats, s);
     else if (want_flat)
         e = launch_ref_tracer(true, a, tiles * 4, depth, stats, s);
-    else
+    else if (lone) {
+        // the lone-pixel kernel on a side stream forked from and joined back into the caller's
+        LoneStreams* ls = lone_streams(s);
+        if (!ls) return set_error("rt_render: cannot create the lone-pixel stream");
+        if (check(hipEventRecord(ls->fork, s), "hipEventRecord") || check(hipStreamWaitEvent(ls->side, ls->fork, 0), "hipStreamWaitEvent"))
+            return 1;
+        e = launch_lone(a, p->lone_slots, (int)p->lone_count, mir.treelets, ls->side);
+        if (e == hipSuccess) e = launch_fast(a, waves, depth, stats, s);
+        if (check(hipEventRecord(ls->join, ls->side), "hipEventRecord") || check(hipStreamWaitEvent(s, ls->join, 0), "hipStreamWaitEvent"))
+            return 1;
+    } else
         e = launch_fast(a, waves, depth, stats, s);
     return check(e, "render_kernel launch");
 }

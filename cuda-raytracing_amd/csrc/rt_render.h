@@ -15,6 +15,8 @@ hipError_t launch_fast_timing(int stack, int mode, const RenderArgs& a, int wave
 hipError_t launch_fast_stats(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);   // 2, 6 (counting)
 hipError_t launch_fast_ab(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);      // 1, 5, 2, 0
 hipError_t launch_fast_refill(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);  // 81, 85
+// The lone-pixel kernel (rt_lone.hip): one wave per slot of `lone_slots`, through the treelets.
+hipError_t launch_lone(const RenderArgs& a, const int32_t* lone_slots, int lone_count, const void* treelets, hipStream_t s);
 // The reference-layout tracer (flat = false) or the exact-division flat tracer (rt_ref.hip).
 hipError_t launch_ref_tracer(bool flat, const RenderArgs& a, int waves, int depth, bool stats, hipStream_t s);
 

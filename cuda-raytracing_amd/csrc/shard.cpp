@@ -116,8 +116,10 @@ extern "C" int64_t rt_lane_plan(const uint32_t* cost, int64_t slots, double para
         return -1;
     }
     const int64_t nw = slots / 64, max_waves = capacity / 64;
+    constexpr uint32_t LONE = 0xffffffffu;  // rt_lone_plan: rendered by the lone-pixel kernel, not here
+    auto cst = [&](int32_t s) { return cost[s] == LONE ? 0.0 : (double)cost[s]; };
     double cmax = 0, csum = 0;
-    for (int64_t s = 0; s < slots; s++) cmax = std::max(cmax, (double)cost[s]), csum += cost[s];
+    for (int64_t s = 0; s < slots; s++) cmax = std::max(cmax, cst((int32_t)s)), csum += cst((int32_t)s);
     const double B = parallel_units > 0 ? slack * std::max(cmax, csum / parallel_units) : 0.0;
     struct Wave {
         std::vector<int32_t> lanes;
@@ -131,8 +133,9 @@ extern "C" int64_t rt_lane_plan(const uint32_t* cost, int64_t slots, double para
         tile[w].order = w;
         for (int l = 0; l < 64; l++) {
             const int32_t s = (int32_t)(w * 64 + l);
+            if (cost[s] == LONE) continue;
             tile[w].lanes.push_back(s);
-            tile[w].mx = std::max(tile[w].mx, (double)cost[s]), tile[w].sum += cost[s];
+            tile[w].mx = std::max(tile[w].mx, cst(s)), tile[w].sum += cst(s);
         }
         e0[w] = wave_units(tile[w].mx, tile[w].sum);
     }
@@ -144,10 +147,10 @@ extern "C" int64_t rt_lane_plan(const uint32_t* cost, int64_t slots, double para
     for (int64_t w : by_e) {
         if (B <= 0 || e0[w] <= B) break;
         std::vector<int32_t> by = tile[w].lanes;
-        std::stable_sort(by.begin(), by.end(), [&](int32_t a, int32_t b) { return cost[a] > cost[b]; });
+        std::stable_sort(by.begin(), by.end(), [&](int32_t a, int32_t b) { return cst(a) > cst(b); });
         std::vector<Wave> sub;
         for (int32_t s : by) {
-            const double c = cost[s];
+            const double c = cst(s);
             bool placed = false;
             for (Wave& v : sub)
                 if (v.lanes.size() < 64 && (c == 0 || wave_units(v.mx, v.sum + c) <= B)) {  // v.mx >= c (decreasing)
@@ -168,8 +171,10 @@ extern "C" int64_t rt_lane_plan(const uint32_t* cost, int64_t slots, double para
     std::vector<Wave> out;
     out.reserve(total);
     for (int64_t w = 0; w < nw; w++) {
-        if (split[w].empty()) out.push_back(std::move(tile[w]));
-        else for (Wave& v : split[w]) out.push_back(std::move(v));
+        if (!split[w].empty())
+            for (Wave& v : split[w]) out.push_back(std::move(v));
+        else if (!tile[w].lanes.empty())  // a sub-tile whose pixels all went to the lone-pixel kernel
+            out.push_back(std::move(tile[w]));
     }
     // long waves (E >= B / 2) first, longest first; then the others in list order
     std::vector<double> e(out.size());
@@ -191,5 +196,24 @@ extern "C" int64_t rt_lane_plan(const uint32_t* cost, int64_t slots, double para
         n += 64;
     }
     if (long_waves) *long_waves = nlong;
+    return n;
+}
+
+// Lone-pixel plans (rt_render_params.lone_slots, rt_lone.hip): the costliest pixels of the probe
+// frame, each to be rendered by a wave of its own, are taken out of the lane plan.
+extern "C" int64_t rt_lone_plan(uint32_t* cost, int64_t slots, int64_t max_lone, uint32_t min_cost, int32_t* lone_slots) {
+    if (!cost || slots <= 0 || slots > ((int64_t)1 << 30) || max_lone < 0 || (max_lone > 0 && !lone_slots)) {
+        rt_internal_set_error("rt_lone_plan: bad arguments");
+        return -1;
+    }
+    std::vector<int32_t> cand;
+    for (int64_t s = 0; s < slots; s++)
+        if (cost[s] != 0xffffffffu && cost[s] >= min_cost && cost[s] > 0) cand.push_back((int32_t)s);
+    std::stable_sort(cand.begin(), cand.end(), [&](int32_t a, int32_t b) { return cost[a] > cost[b]; });
+    const int64_t n = std::min<int64_t>(max_lone, (int64_t)cand.size());
+    for (int64_t i = 0; i < n; i++) {
+        lone_slots[i] = cand[i];
+        cost[cand[i]] = 0xffffffffu;
+    }
     return n;
 }

@@ -200,6 +200,14 @@ typedef struct rt_render_params {
      * 16.9 ms), slower on others (config 4: 95 vs 90 ms); bench.py picks it per configuration by
      * timing one untimed probe frame of each.  Any other value is an error. */
     int32_t waves_per_simd;
+    /* Lone pixels (production tracer; rt_lone.hip): DEVICE int32 slots (the lane_slots numbering)
+     * that the lone-pixel kernel renders one per wave -- all 64 lanes on the pixel's one ray, the BVH
+     * read as treelets -- concurrently with the production kernel on a second stream joined back
+     * into `stream`.  Requires lane_slots, which must not hold these slots (rt_lone_plan picks them
+     * and marks them for rt_lane_plan).  Bit-identical pixels either way; it shortens the chains
+     * of a strong-scaled frame's costliest pixels.  lone_count 0 = none. */
+    const int32_t* lone_slots;
+    int64_t lone_count;
 } rt_render_params;
 
 /* Layout rule: with out_shard set, RNG state s and output s are compact in list order
@@ -290,12 +298,17 @@ int64_t rt_lane_plan_capacity(int64_t slots);
  * max c x (sum c / max c)^0.34 work units; every 8x8 sub-tile wave above the target
  * slack x max(max c, sum c / parallel_units) is split (first fit, heaviest pixels first) into
  * sub-waves within it.  Waves of at least half the target go first, longest first; the rest keep
- * list order.  parallel_units <= 0: the identity map.  MI355X: 48000 (bench.py --lane-units; measured
+ * list order.  Slots whose cost is UINT32_MAX (rt_lone_plan's lone pixels) are left out of the map.  parallel_units <= 0: the identity map.  MI355X: 48000 (bench.py --lane-units; measured
  * best for configs 2 and 3 at N = 2-8).
  * *long_waves (optional) receives the number of those leading waves (rt_render_params.
  * priority_waves).  Returns the entries written (a multiple of 64), or -1 on bad arguments. */
 int64_t rt_lane_plan(const uint32_t* cost, int64_t slots, double parallel_units, double slack,
                      int32_t* lane_slots, int64_t capacity, int64_t* long_waves);
+/* Lone-pixel plans: write to HOST lone_slots (up to max_lone entries) the slots whose probe work
+ * `cost` is at least min_cost, heaviest first (ties: lower slot first), and mark each of them in
+ * `cost` with UINT32_MAX -- the value rt_lane_plan treats as "not in this map".  Returns the number
+ * written, or -1 on bad arguments. */
+int64_t rt_lone_plan(uint32_t* cost, int64_t slots, int64_t max_lone, uint32_t min_cost, int32_t* lone_slots);
 /* rt_init_rng for an explicit tile list (DEVICE int32): state k*256 + t <- curand_init(seed,
  * pixel id of thread t of tile tile_list[k]). */
 int rt_init_rng_tiles(void* rng_states, int width, int height, const int32_t* tile_list, int64_t tile_count,

@@ -232,3 +232,38 @@ def test_launcher_deadline_kills_stalled_job():
     assert procs[1].returncode == 124 and "deadline exceeded in phase 'collective'" in out[1]
     assert procs[0].returncode != 0
     assert time.monotonic() - t0 < 90
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_gather_bookkeeping_uneven_shards(world):
+    """The RCCL gather's byte bookkeeping without a transfer (the multi-rank send/recv group itself
+    has only run with one rank and in same-GPU rehearsals): bench.gather_layout's recv_bytes and
+    stride for an LPT plan with uneven tile counts, rt_gather_shards' copy rule restated (rank r's
+    first recv_bytes[r] bytes land at r * stride; the rest of row r keeps whatever the buffer held),
+    then the unshard -- the frame comes back exactly, and no slot past a rank's counts[r] tiles is
+    ever read (they hold NaN here)."""
+    import bench
+
+    rt = T.load_rt()
+    sh = rt.sharding
+    w, h = 200, 120
+    rng = np.random.default_rng(world)
+    frame = rng.random((h, w, 4), dtype=np.float32)
+    tiles = sh.tiles_total(w, h)
+    cost = rng.gamma(0.3, 1.0, tiles) * np.where(rng.random(tiles) < 0.1, 30.0, 1.0)
+    lists, counts = rt.shard_plan(w, h, world, cost)
+    cap = lists.shape[1]
+    assert len(set(counts.tolist())) > 1 or world == 1, "the plan should be uneven for this test"
+    recv_bytes, stride = bench.gather_layout(counts, cap)
+    assert stride == cap * 256 * 16 and all(rb <= stride for rb in recv_bytes)
+    gathered = np.full((world, stride // 4), np.nan, dtype=np.float32)  # the root's buffer, never cleared
+    for r in range(world):
+        shard = np.full((cap * 256, 4), np.nan, dtype=np.float32)  # a rank's whole shard buffer
+        xs, ys = sh.slot_pixels(w, h, r, world, cap, lists[r, : counts[r]])
+        ok = xs >= 0
+        shard[ok] = frame[ys[ok], xs[ok]]
+        n = recv_bytes[r] // 4
+        gathered[r, :n] = shard.reshape(-1)[:n]  # rt_gather_shards: recv_bytes[r] bytes at r * stride
+    img, seen = unshard_host(gathered.reshape(world, cap * 256, 4), w, h, lists)
+    assert (seen == 1).all()
+    assert np.array_equal(img, frame)

@@ -317,3 +317,75 @@ def test_short_buffers_are_refused(rt):
     with pytest.raises(rt.RTError):
         rt.unshard_tiles(a, w, h, torch.zeros((2, 256, 4), device="cuda"), torch.from_numpy(lists).cuda())
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("which,frac", [("bunny", 0.25), ("bunny", 1.0), ("bunny4", 0.3)])
+def test_lone_pixels_equal_full(rt, which, frac):
+    """rt_lone_plan + the lone-pixel kernel (rt_lone.hip: one wave per pixel, the BVH walked as
+    treelets by ballots over their preorder slots) beside the production kernel's lane map: the
+    frames and the RNG progression over two progressive frames equal the plain render bit for bit.
+    frac = the share of the frame's pixels (heaviest first) that go to the lone-pixel kernel; the
+    4-bunny scene brings leaf trees (coop_tree) into the lone walk."""
+    w, h, spp, bounces = 120, 72, 2, 6
+    full, rng_full = full_frames(rt, w, h, spp, bounces, 2, which)
+    s = scene(rt, w, h, which)
+    tiles = rt.sharding.tiles_total(w, h)
+    mine = torch.arange(tiles, dtype=torch.int32, device="cuda")
+    c = lane_costs(rt, s, w, h, spp, bounces, mine, 1, 0)
+    inside = int((c > 0).sum())
+    lone, marked = rt.lone_plan(c, max(1, int(frac * inside)))
+    assert lone.size == max(1, int(frac * inside)) and (c[lone] >= np.sort(c[c > 0])[::-1][lone.size - 1]).all()
+    m, nlong = rt.lane_plan(marked, 48000.0, 1.0)
+    assert not np.isin(m, lone).any(), "the lane map leaves the lone pixels out"
+    assert np.array_equal(np.sort(np.concatenate([m[m >= 0], lone])), np.sort(np.flatnonzero(np.arange(c.size) >= 0)))
+    lm = torch.from_numpy(m if m.size else np.full(64, -1, np.int32)).cuda()
+    rng = rt.alloc_rng(w * h)
+    rt.init_rng_states(rng, w, h, T.SEED)
+    s.upload(rng.data_ptr())
+    bufs = [rt.alloc_surface(w, h), rt.alloc_surface(w, h)]
+    lo = torch.from_numpy(lone).cuda()
+    for f in range(2):
+        rt.render(s, bufs[f & 1], bufs[(f + 1) & 1], w, h, spp, bounces, f, tile_list=mine, lane_slots=lm,
+                  priority_waves=nlong, lone_slots=lo)
+    torch.cuda.synchronize()
+    got = rt.surface_view(bufs[1], w).cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), full.view(np.uint32)), f"{which} frac={frac}"
+    assert np.array_equal(rng.cpu().numpy(), rng_full)
+
+
+def test_lone_pixels_config2_full_frame(rt):
+    """Config 2 at full size (1920x1080, 8 spp, 6 bounces) with its 4096 costliest pixels in the
+    lone-pixel kernel: bit-identical to the plain production frame, RNG states included."""
+    w, h, spp, bounces = 1920, 1080, 8, 6
+    full, rng_full = full_frames(rt, w, h, spp, bounces, 1)
+    s = scene(rt, w, h)
+    tiles = rt.sharding.tiles_total(w, h)
+    mine = torch.arange(tiles, dtype=torch.int32, device="cuda")
+    c = lane_costs(rt, s, w, h, spp, bounces, mine, 1, 0)
+    lone, marked = rt.lone_plan(c, 4096)
+    m, nlong = rt.lane_plan(marked, 48000.0, 1.0)
+    rng = rt.alloc_rng(w * h)
+    rt.init_rng_states(rng, w, h, T.SEED)
+    s.upload(rng.data_ptr())
+    a, b = rt.alloc_surface(w, h), rt.alloc_surface(w, h)
+    rt.render(s, a, b, w, h, spp, bounces, 0, tile_list=mine, lane_slots=torch.from_numpy(m).cuda(),
+              priority_waves=nlong, lone_slots=torch.from_numpy(lone).cuda())
+    torch.cuda.synchronize()
+    got = rt.surface_view(a, w).cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), full.view(np.uint32))
+    assert np.array_equal(rng.cpu().numpy(), rng_full)
+
+
+def test_lone_misuse_is_refused(rt):
+    w, h = 64, 64
+    s = scene(rt, w, h)
+    rng = rt.alloc_rng(w * h)
+    rt.init_rng_states(rng, w, h, T.SEED)
+    s.upload(rng.data_ptr())
+    a, b = rt.alloc_surface(w, h), rt.alloc_surface(w, h)
+    lo = torch.zeros(4, dtype=torch.int32, device="cuda")
+    with pytest.raises(rt.RTError, match="lone"):
+        rt.render(s, a, b, w, h, 1, 1, lone_slots=lo)  # no lane map
+    with pytest.raises(rt.RTError, match="production tracer"):
+        rt.render(s, a, b, w, h, 1, 1, tracer="ref", lone_slots=lo, lane_slots=torch.full((64,), -1, dtype=torch.int32, device="cuda"))
+    torch.cuda.synchronize()

@@ -90,3 +90,27 @@ def test_bad_arguments(rt):
         rt.lane_plan(np.ones(100, dtype=np.uint32), 1.0, 1.0)  # not a multiple of 64
     with pytest.raises(rt.RTError, match="lane_plan"):
         rt.lane_plan(np.ones(64, dtype=np.uint32), 1.0, 0.0)  # slack must be > 0
+
+
+def test_lone_plan_takes_the_heaviest_and_lane_plan_skips_them(rt):
+    """rt_lone_plan picks the costliest slots (heaviest first, ties by slot), at least min_cost,
+    at most max_lone, and marks them UINT32_MAX; rt_lane_plan then maps every other slot exactly
+    once and none of the lone ones (sub-tile waves emptied by it disappear)."""
+    gen = np.random.default_rng(3)
+    cost = gen.integers(1, 1000, 64 * 50).astype(np.uint32)
+    cost[64 * 7: 64 * 8] = 5000  # a sub-tile taken whole
+    lone, marked = rt.lone_plan(cost, 100, 1)
+    assert lone.size == 100 and (marked[lone] == 0xFFFFFFFF).all()
+    assert list(cost[lone]) == sorted(cost[lone], reverse=True)
+    assert cost[lone].min() >= np.delete(cost, lone).max()
+    assert set(range(64 * 7, 64 * 8)) <= set(lone.tolist())
+    rest = np.setdiff1d(np.arange(cost.size), lone)
+    for units in (0.0, 48000.0, 1e12):
+        m, _ = rt.lane_plan(marked, units, 1.0)
+        v = m[m >= 0]
+        assert np.array_equal(np.sort(v), rest), units
+        assert not (m.reshape(-1, 64) < 0).all(axis=1).any(), "no empty waves"
+    few, _ = rt.lone_plan(cost, 10, 4000)
+    assert few.size == 10 and (cost[few] == 5000).all()
+    none, same = rt.lone_plan(cost, 10, 6000)
+    assert none.size == 0 and np.array_equal(same, cost)

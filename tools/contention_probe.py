@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--units", type=float, default=48000.0)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--lone", type=lambda x: [int(v) for v in x.split(",") if v], default=[256, 1024])
     args = ap.parse_args()
     rt = G.load_package()
     scene_name, W, H, SPP, BOUNCES, _ = bench.CONFIGS[args.config]
@@ -55,15 +56,16 @@ def main():
     res = {"config": args.config, "n": args.n, "rank": args.rank, "waves": int(lm.size // 64), "long_waves": int(nlong),
            "even_share_ms": None}
 
-    def timed(m, wps, prio):
+    def timed(m, wps, prio, lone=None):
         d = torch.from_numpy(np.ascontiguousarray(m)).cuda()
+        lo = None if lone is None else torch.from_numpy(np.ascontiguousarray(lone, dtype=np.int32)).cuda()
         ms = []
         for i in range(args.reps + 1):
             rng.copy_(saved)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             rt.render(scene, None, None, W, H, SPP, BOUNCES, 0, out_shard=out, tile_list=mine, lane_slots=d,
-                      priority_waves=prio, waves_per_simd=wps)
+                      priority_waves=prio, waves_per_simd=wps, lone_slots=lo)
             e1.record()
             torch.cuda.synchronize()
             if i:
@@ -77,6 +79,15 @@ def main():
     # the unplanned shard (sub-tile waves in list order) for reference
     ident = np.arange(slots, dtype=np.int32)
     res["no_lane_plan_w6_ms"] = timed(ident, 6, 0)
+    # lone pixels (rt_lone_plan): the main kernel without them, the lone kernel alone, both together
+    idle = np.full(64, -1, dtype=np.int32)
+    for k in args.lone:
+        lone, marked = rt.lone_plan(c, k)
+        lmk, nl = rt.lane_plan(marked, args.units, 1.0)
+        res[f"lone{k}_main_only_ms"] = timed(lmk, 6, 0)
+        res[f"lone{k}_lone_only_ms"] = timed(idle, 6, 0, lone)
+        res[f"lone{k}_both_ms"] = timed(lmk, 6, 0, lone)
+        res[f"lone{k}_main_waves"] = int(lmk.size // 64)
     print(json.dumps(res), flush=True)
 
 

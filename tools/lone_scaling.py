@@ -49,15 +49,16 @@ def main():
     wave_of = c.reshape(-1, 64).max(1)
     topw = int(np.argmax(c.reshape(-1, 64).sum(1)))  # the 8x8 sub-tile with the most work
 
-    def timed(m, wps=6):
+    def timed(m, wps=6, lone=None):
         d = torch.from_numpy(np.ascontiguousarray(m, dtype=np.int32)).cuda()
+        lo = None if lone is None else torch.from_numpy(np.ascontiguousarray(lone, dtype=np.int32)).cuda()
         ms = []
         for i in range(3):
             rng.copy_(saved)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             rt.render(scene, None, None, W, H, SPP, BOUNCES, 0, out_shard=out, tile_list=mine, lane_slots=d,
-                      waves_per_simd=wps, tune=args.tune)
+                      waves_per_simd=wps, tune=args.tune, lone_slots=lo)
             e1.record()
             torch.cuda.synchronize()
             if i:
@@ -69,10 +70,18 @@ def main():
     full = np.arange(topw * 64, topw * 64 + 64, dtype=np.int32)
     res = {"config": args.config, "pixel_slot": top, "pixel_work": int(c[top]), "subtile": topw,
            "subtile_work_sum": int(c[topw * 64:(topw + 1) * 64].sum()), "subtile_work_max": int(wave_of[topw])}
+    idle = np.full(64, -1, dtype=np.int32)
     for k in map(int, args.ks.split(",")):
         res[f"pixel_x{k}_ms"] = timed(np.tile(one, k))
         res[f"subtile_x{k}_ms"] = timed(np.tile(full, k))
-        print(json.dumps({"k": k, "pixel_ms": res[f"pixel_x{k}_ms"], "subtile_ms": res[f"subtile_x{k}_ms"]}), flush=True)
+        # the same work through the lone-pixel kernel (rt_lone.hip): K copies of the pixel, and the
+        # sub-tile's 64 pixels K times, one wave per pixel
+        res[f"lone_pixel_x{k}_ms"] = timed(idle, lone=np.full(k, top, dtype=np.int32))
+        if k <= 1024:
+            res[f"lone_subtile_x{k}_ms"] = timed(idle, lone=np.tile(full, k))
+        print(json.dumps({"k": k, "pixel_ms": res[f"pixel_x{k}_ms"], "subtile_ms": res[f"subtile_x{k}_ms"],
+                          "lone_pixel_ms": res[f"lone_pixel_x{k}_ms"],
+                          "lone_subtile_ms": res.get(f"lone_subtile_x{k}_ms")}), flush=True)
     print(json.dumps(res), flush=True)
 
 

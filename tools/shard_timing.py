@@ -37,7 +37,7 @@ def probe(rt, scene, W, H, SPP, BOUNCES):
     return cost
 
 
-TUNE, WPS, SPLIT = 0, 0, 1  # --tune / --wps / --split
+TUNE, WPS, SPLIT, LONE, LONE_MIN = 0, 0, 1, 0, 1  # --tune / --wps / --split / --lone / --lone-min
 
 
 def lane_map(rt, scene, W, H, SPP, BOUNCES, mine, rng, lane):
@@ -51,6 +51,10 @@ def lane_map(rt, scene, W, H, SPP, BOUNCES, mine, rng, lane):
     if os.environ.get("LANE_SAVE"):  # per-slot probe costs for offline plan work
         os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
         np.save(os.path.join(ROOT, "gpurun_out", f"lanecost_{os.environ['LANE_SAVE']}_{mine.numel()}_{int(mine[0])}.npy"), c)
+    lone = None
+    if LONE:  # the costliest pixels to the lone-pixel kernel (rt_lone_plan), the rest through the lane plan
+        lone_np, c = rt.lone_plan(c, LONE, LONE_MIN)
+        lone = torch.from_numpy(lone_np).cuda() if lone_np.size else None
     m, nlong = rt.lane_plan(c, lane[0], lane[1])
     nlong = int(lane[2]) if len(lane) >= 3 else nlong  # lane[2]: the number of leading waves at raised priority
     rt.init_rng_tiles(rng, W, H, mine, bench.SEED)
@@ -70,7 +74,7 @@ def lane_map(rt, scene, W, H, SPP, BOUNCES, mine, rng, lane):
                           "top_waves": [[int(i), round(float(wc[i]) / 1e5, 3), int((mw[i] >= 0).sum()),
                                          int(c[mw[i][mw[i] >= 0]].max()), int(c[mw[i][mw[i] >= 0]].sum())] for i in top]}),
               flush=True)
-    return lm, nlong
+    return lm, nlong, lone
 
 
 def time_shard(rt, scene, W, H, SPP, BOUNCES, tiles, r, n, reps, lane=None):
@@ -78,7 +82,7 @@ def time_shard(rt, scene, W, H, SPP, BOUNCES, tiles, r, n, reps, lane=None):
     rng = rt.alloc_rng(len(tiles) * 256)
     rt.init_rng_tiles(rng, W, H, mine, bench.SEED)
     scene.upload(rng.data_ptr())
-    lm, nlong = lane_map(rt, scene, W, H, SPP, BOUNCES, mine, rng, lane) if lane else (None, 0)
+    lm, nlong, lone = lane_map(rt, scene, W, H, SPP, BOUNCES, mine, rng, lane) if lane else (None, 0, None)
     if SPLIT > 1:  # every 8x8 wave split into SPLIT waves of 64 / SPLIT pixels (rows of the sub-tile)
         slots = np.arange(len(tiles) * 256, dtype=np.int32).reshape(-1, SPLIT, 64 // SPLIT)
         m = np.full((slots.shape[0] * SPLIT, 64), -1, dtype=np.int32)
@@ -90,7 +94,7 @@ def time_shard(rt, scene, W, H, SPP, BOUNCES, tiles, r, n, reps, lane=None):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         rt.render(scene, None, bufs[(i + 1) & 1], W, H, SPP, BOUNCES, i, r, n, out_shard=bufs[i & 1], tile_list=mine,
-                  lane_slots=lm, priority_waves=nlong, tune=TUNE, waves_per_simd=WPS)
+                  lane_slots=lm, priority_waves=nlong, tune=TUNE, waves_per_simd=WPS, lone_slots=lone)
         e1.record()
         torch.cuda.synchronize()
         if i:
@@ -109,17 +113,21 @@ def main():
     ap.add_argument("--tune", type=lambda x: int(x, 0), default=0, help="diagnostic A/B knobs passed to rt_render")
     ap.add_argument("--wps", type=int, default=0, help="rt_render waves_per_simd (0 = default)")
     ap.add_argument("--split", type=int, default=1, help="split every 8x8 wave into this many waves (1, 2, 4)")
+    ap.add_argument("--lone", default="0", help="comma list of lone-pixel counts per shard to try (rt_lone_plan)")
+    ap.add_argument("--lone-min", type=int, default=1, help="rt_lone_plan min_cost")
     args = ap.parse_args()
-    global TUNE, WPS, SPLIT
-    TUNE, WPS, SPLIT = args.tune, args.wps, args.split
+    global TUNE, WPS, SPLIT, LONE, LONE_MIN
+    TUNE, WPS, SPLIT, LONE_MIN = args.tune, args.wps, args.split, args.lone_min
+    lone_list = [int(x) for x in args.lone.split(",")]
     rt = G.load_package()
     scene_name, W0, H0, SPP, BOUNCES, _ = bench.CONFIGS[args.config]
     torch.cuda.set_device(0)
     res = {"config": args.config, "weak": args.weak, "plans": {}}
     costs = {}
     lanes = [None] + [tuple(map(float, x.split(":"))) for x in args.lanes.split(";") if x]
-    plans = [(p, l) for p in args.plans.split(",") for l in lanes]
-    for plan, lane in plans:
+    plans = [(p, l, k) for p in args.plans.split(",") for l in lanes for k in (lone_list if l else [0])]
+    for plan, lane, lone_k in plans:
+        LONE = lone_k
         per_n = {}
         for n in map(int, args.ns.split(",")):
             W, H = bench.weak_size(W0, H0, n) if args.weak else (W0, H0)
@@ -135,10 +143,10 @@ def main():
             shard_ms = [time_shard(rt, scene, W, H, SPP, BOUNCES, lists[r, : counts[r]], r, n, args.reps, lane)
                         for r in range(n)]
             per_n[n] = shard_ms
-            print(json.dumps({"plan": plan, "lane": lane, "n": n, "max_ms": round(max(shard_ms), 3),
+            print(json.dumps({"plan": plan, "lane": lane, "lone": lone_k, "n": n, "max_ms": round(max(shard_ms), 3),
                               "shard_ms": [round(x, 3) for x in shard_ms]}), flush=True)
         t1 = max(per_n[min(per_n)])
-        res["plans"][plan + ("" if lane is None else f" lane{lane}")] = {"max_shard_ms": {str(n): round(max(v), 3) for n, v in per_n.items()},
+        res["plans"][plan + ("" if lane is None else f" lane{lane}") + (f" lone{lone_k}" if lone_k else "")] = {"max_shard_ms": {str(n): round(max(v), 3) for n, v in per_n.items()},
                               "shard_ms": {str(n): [round(x, 3) for x in v] for n, v in per_n.items()},
                               "compute_speedup": {str(n): round((n if args.weak else 1) * t1 / max(v), 2)
                                                   for n, v in per_n.items()}}

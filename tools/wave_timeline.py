@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--units", type=float, default=48000.0)
     ap.add_argument("--tune", type=lambda x: int(x, 0), default=0)
+    ap.add_argument("--lone", type=int, default=0, help="pixels to the lone-pixel kernel (timing frame: left out)")
     args = ap.parse_args()
     rt = G.load_package()
     scene_name, W, H, SPP, BOUNCES, _ = bench.CONFIGS[args.config]
@@ -48,6 +49,10 @@ def main():
     rt.render(scene, None, None, W, H, SPP, BOUNCES, 0, out_shard=out, tile_list=mine, lane_cost=pc)
     torch.cuda.synchronize()
     c = pc.cpu().numpy()
+    lone = None
+    if args.lone:  # the costliest pixels to the lone-pixel kernel (rt_lone_plan), the rest through the lane plan
+        lone_np, c = rt.lone_plan(c, args.lone)
+        lone = torch.from_numpy(lone_np).cuda()
     lm, nlong = rt.lane_plan(c, args.units, 1.0)
     rt.init_rng_tiles(rng, W, H, mine, bench.SEED)
     lmd = torch.from_numpy(lm).cuda()
@@ -59,7 +64,7 @@ def main():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         rt.render(scene, None, None, W, H, SPP, BOUNCES, 0, out_shard=out, tile_list=mine, lane_slots=lmd,
-                  stats=st if tune else None, tune=tune | args.tune)
+                  stats=st if tune else None, tune=tune | args.tune, lone_slots=None if tune else lone)
         e1.record()
         torch.cuda.synchronize()
         res[label] = e0.elapsed_time(e1)
@@ -73,7 +78,7 @@ def main():
     cmax = np.array([c[r[r >= 0]].max() if (r >= 0).any() else 0 for r in mw])
     csum = np.array([c[r[r >= 0]].sum() if (r >= 0).any() else 0 for r in mw])
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    np.savez(os.path.join(ROOT, "gpurun_out", f"timeline_{args.config}_n{args.n}_r{args.rank}.npz"), start=start, end=end,
+    np.savez(os.path.join(ROOT, "gpurun_out", f"timeline_{args.config}_n{args.n}_r{args.rank}_l{args.lone}.npz"), start=start, end=end,
              npx=npx, cmax=cmax, csum=csum, small=t[:, 2], big=t[:, 3], iters=t[:, 5], wsmall=t[:, 6], lsmall=t[:, 7],
              lane_cost=c, lane_map=lm)
     top = np.argsort(-end)[:10]
