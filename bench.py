@@ -254,6 +254,8 @@ def pmc_pass(args, out_dir, timeout_s=150):
                "--lanes", args.lanes, "--lane-units", str(args.lane_units), "--occupancy", str(args.occupancy_chosen)]
         if args.foreign:
             cmd.append("--foreign")
+        if args.build_options:
+            cmd += ["--build-options", args.build_options]
         try:
             r = subprocess.run(cmd, cwd=tempfile.gettempdir(), capture_output=True, text=True, timeout=timeout_s,
                                env=dict(os.environ, TMPDIR=tempfile.gettempdir()))
@@ -447,6 +449,9 @@ def run(args):
     wd.phase = "scene set-up and plans"
     assert world == args.gpus or args.pmc_child, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     rt = G.load_package()
+    if args.build_options:  # exact-preserving mirror / BVH builder knobs (rt_set_build_options)
+        rt.set_build_options(**{k: float(v) if k == "split_angle" else int(v)
+                                for k, v in (kv.split("=") for kv in args.build_options.split(","))})
     scene_name, W, H, SPP, BOUNCES, desc = CONFIGS[args.config]
     if world > 1 and args.scaling == "weak":
         W, H = weak_size(W, H, world)
@@ -787,6 +792,8 @@ def main():
     ap.add_argument("--foreign", action="store_true",
                     help="render a GPUScene filled outside this library (the reference's Scene::Upload pattern): "
                          "fingerprint-gated mirror, no host synchronisation per frame")
+    ap.add_argument("--build-options", default="",
+                    help="rt_set_build_options fields, e.g. leaf_tree_min=300,cluster_max=16 (exact-preserving A/B)")
     ap.add_argument("--rank-deadline", type=float, default=480.0,
                     help="N > 1: seconds after which a still-running job is killed whole (0 = none)")
     ap.add_argument("--check", action="store_true",

@@ -29,7 +29,9 @@ __device__ __forceinline__ bool shade_segment(const RenderArgs& a, const rtfast:
                                               const rtm::f3 nd, rtm::Xorwow& rng, rtm::f3& color, rtm::f3& thr,
                                               Counters& c) {
     bool end = false;
-    if (h.kind != 0) {
+    // GetRayHit returns `result.distance < max_distance` (main_raytracing.cu:108): a hit whose
+    // accepted distance is NaN counts as a miss, as in the reference
+    if (h.kind != 0 && h.best < 1e30f) {
         if (STATS) c.hit++;
         const rtm::f3 pos = rtm::add(ro, rtm::muls(nd, h.best));
         rtm::f3 nrm;

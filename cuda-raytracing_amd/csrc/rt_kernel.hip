@@ -336,8 +336,16 @@ __global__ __launch_bounds__(BLOCK) void fingerprint_kernel(HashArrays h, unsign
         for (unsigned long long i = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x; i < h.n[k]; i += stride)
             acc += mix64(((unsigned long long)k << 60) ^ (i << 32) ^ h.w[k][i]);
     }
+    // one atomic per workgroup (the per-wave atomics on one word serialised: 55 us per frame)
+    __shared__ unsigned long long part[BLOCK / 64];
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-    if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < BLOCK / 64; w++) t += part[w];
+        atomicAdd(out, t);
+    }
 }
 
 // flag = (fingerprint == expected) for the gated launches; then clears the accumulator for the
@@ -533,7 +541,7 @@ static int foreign_frame(const GPUScene* scene, hipStream_t st, MirrorDevice* mi
     h.w[1] = scene->gpu_bvh_face_indices, h.n[1] = bytes[1] / 4;
     h.w[2] = (const uint32_t*)scene->gpu_faces, h.n[2] = bytes[2] / 4;
     h.w[3] = (const uint32_t*)scene->gpu_vertices, h.n[3] = bytes[3] / 4;
-    hipLaunchKernelGGL(fingerprint_kernel, dim3(1024), dim3(BLOCK), 0, st, h, fe->d_acc);
+    hipLaunchKernelGGL(fingerprint_kernel, dim3(512), dim3(BLOCK), 0, st, h, fe->d_acc);
     hipLaunchKernelGGL(fingerprint_gate_kernel, dim3(1), dim3(1), 0, st, fe->d_acc, salt, (unsigned long long)fe->fp_mirror,
                        fe->have ? 1 : 0, fe->d_flag, fe->d_fp);
     if (!fe->fp_pending) {

@@ -205,7 +205,9 @@ __device__ __forceinline__ void shade_pixel(const RenderArgs& a, uint32_t* stk, 
             trace_spheres<STATS>(a, ro, nd, h, c);
             Tracer::template trace<STACK, STATS>(a, stk, ro, rd, nd, h, c);
 
-            if (h.kind != 0) {
+            // GetRayHit returns `result.distance < max_distance` (main_raytracing.cu:108): a hit whose
+            // accepted distance is NaN counts as a miss, as in the reference
+            if (h.kind != 0 && h.best < 1e30f) {
                 if (STATS) c.hit++;
                 // Attributes of the final closest hit (the reference recomputes them on every
                 // accept; only the last accept survives, so computing them once is identical).
