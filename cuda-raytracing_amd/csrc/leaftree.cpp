@@ -224,19 +224,28 @@ void rt_build_leaf_flat(std::vector<float>& nodes, uint32_t root, const LeafTree
     const uint32_t end = u32(root, 13);
     // clusters in pre-order; first_cluster[k - root] = clusters before node k
     std::vector<uint32_t> first_cluster(end - root + 1, 0);
-    const uint32_t cbase = (uint32_t)(flat.size() / 16);
+    // records are appended field-major (leaftree.h): field f of record i of a list of n at
+    // float4 index base + f * n + i
+    auto append_soa = [&](const std::vector<float>& recs) {
+        const size_t n = recs.size() / 16;
+        for (int f = 0; f < 4; f++)
+            for (size_t i = 0; i < n; i++) flat.insert(flat.end(), &recs[i * 16 + 4 * f], &recs[i * 16 + 4 * f] + 4);
+    };
+    const uint32_t cbase = (uint32_t)(flat.size() / 4);
     uint32_t nc = 0;
+    std::vector<float> crec;
     for (uint32_t k = root; k < end; k++) {
         first_cluster[k - root] = nc;
         if (u32(k, 14) != ~0u) {
-            const size_t o = flat.size();
-            flat.insert(flat.end(), &nodes[(size_t)k * 16], &nodes[(size_t)k * 16] + 16);
-            put(&flat[o], 13, cbase + nc + 1);
+            const size_t o = crec.size();
+            crec.insert(crec.end(), &nodes[(size_t)k * 16], &nodes[(size_t)k * 16] + 16);
+            put(&crec[o], 13, nc + 1);
             nc++;
         }
     }
+    append_soa(crec);
     first_cluster[end - root] = nc;
-    const uint32_t kbase = (uint32_t)(flat.size() / 16);
+    const uint32_t kbase = (uint32_t)(flat.size() / 4);
     uint32_t nk = 0;
     std::vector<uint32_t> todo{root};
     std::vector<uint32_t> cuts;
@@ -254,13 +263,15 @@ void rt_build_leaf_flat(std::vector<float>& nodes, uint32_t root, const LeafTree
         for (uint32_t c = k + 1; c < skip; c = u32(c, 13)) ch.push_back(c);
         for (auto it = ch.rbegin(); it != ch.rend(); ++it) todo.push_back(*it);
     }
+    std::vector<float> krec;
     for (uint32_t k : cuts) {
-        const size_t o = flat.size();
-        flat.insert(flat.end(), &nodes[(size_t)k * 16], &nodes[(size_t)k * 16] + 16);
-        put(&flat[o], 13, first_cluster[k - root]);
-        put(&flat[o], 14, first_cluster[u32(k, 13) - root]);
+        const size_t o = krec.size();
+        krec.insert(krec.end(), &nodes[(size_t)k * 16], &nodes[(size_t)k * 16] + 16);
+        put(&krec[o], 13, first_cluster[k - root]);
+        put(&krec[o], 14, first_cluster[u32(k, 13) - root]);
         nk++;
     }
+    append_soa(krec);
     float* R = &nodes[(size_t)root * 16];
     put(R, 8, cbase);
     put(R, 9, nc);

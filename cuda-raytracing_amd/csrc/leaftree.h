@@ -25,9 +25,14 @@
 //   cuts      a cut of the tree into subtrees of at most LeafTreeParams::cut_clusters clusters:
 //             copies of those nodes with K3.y = first cluster, K3.z = end cluster (the
 //             subtree's clusters are contiguous in pre-order).
+// Both lists are stored field-major: field Kf of record i of a list of n records at float4
+// index base + f * n + i.  The walk reads one field of 32-64 consecutive records per load
+// instruction, so an instruction touches 4-8 cache lines instead of 32 (the CU's load path
+// spends about a cycle per line beyond 16 per instruction; tools/td_microbench.hip).
 // The root records where they are: K2 = (cluster base, cluster count, cut base, cut count) in
-// 16-float units of the flat array (uint bits) and info bit 1 set; the root is never culled, so
-// its cone fields are free.
+// float4 units of the flat array (uint bits) and info bit 1 set; the root is never culled, so
+// its cone fields are free: K3.x holds the record count of the leaf-tree triangle array, which the
+// device holds field-major too (record i: A at i, B at n + i, C at 2n + i; mirror.cpp).
 #pragma once
 
 #include <cstdint>

@@ -85,6 +85,7 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
     }
     std::sort(big.begin(), big.end());
     big.erase(std::unique(big.begin(), big.end()), big.end());
+    std::vector<uint32_t> roots;
     for (uint32_t n : big) {
         const GPUBVHNode& nd = nodes[n];
         float* lead = &out->tris[(size_t)nd.first_index * 12];
@@ -103,6 +104,7 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
             po = rt_build_leaf_tree(&out->tris[(size_t)nd.first_index * 12], nd.prim_count, prm, out->tree, out->ltris);
             rt_build_leaf_flat(out->tree, po, prm, out->flat);
             if (out->ltris.size() / 12 >= (1u << 26)) bad("leaf trees too large (record index >= 2^26)");
+            roots.push_back(po);
             pf = 2;
             std::memcpy(&lead[10], &po, 4);
             std::memcpy(&lead[11], &pf, 4);
@@ -119,7 +121,18 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
             out->pairs.insert(out->pairs.end(), q, q + 20);
         }
     }
+    // every root's K3.x: the leaf-tree triangle count, the stride of their field-major device copy
+    const uint32_t nl = (uint32_t)(out->ltris.size() / 12);
+    for (uint32_t r : roots) std::memcpy(&out->tree[(size_t)r * 16 + 12], &nl, 4);
     rt_build_treelets(nodes, node_count, out->treelets);
+}
+
+std::vector<float> rt_ltris_device_layout(const std::vector<float>& ltris) {
+    const size_t n = ltris.size() / 12;
+    std::vector<float> d(ltris.size());
+    for (size_t i = 0; i < n; i++)
+        for (int f = 0; f < 3; f++) std::memcpy(&d[(f * n + i) * 4], &ltris[i * 12 + 4 * f], 16);
+    return d;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -213,13 +226,14 @@ void release(Entry& e) {
 int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owned, uint64_t fingerprint) {
     const size_t nt = m.tris.size() * 4, np = m.pairs.size() * 4, nk = m.tree.size() * 4, nl = m.ltris.size() * 4,
                  ns = m.spairs.size() * 4, nf = m.flat.size() * 4, nq = m.treelets.size() * 4;
+    const std::vector<float> lt = rt_ltris_device_layout(m.ltris);
     void* block = nullptr;
     if (rt_malloc(&block, nt + np + nk + nl + ns + nf + nq + 64) != 0) return -1;
     char* b = static_cast<char*>(block);
     const size_t oq = nt + np + nk + nl + ns + nf;
     if ((nt && rt_memcpy_h2d(b, m.tris.data(), nt) != 0) || (np && rt_memcpy_h2d(b + nt, m.pairs.data(), np) != 0) ||
         (nk && rt_memcpy_h2d(b + nt + np, m.tree.data(), nk) != 0) ||
-        (nl && rt_memcpy_h2d(b + nt + np + nk, m.ltris.data(), nl) != 0) ||
+        (nl && rt_memcpy_h2d(b + nt + np + nk, lt.data(), nl) != 0) ||
         (ns && rt_memcpy_h2d(b + nt + np + nk + nl, m.spairs.data(), ns) != 0) ||
         (nf && rt_memcpy_h2d(b + nt + np + nk + nl + ns, m.flat.data(), nf) != 0) ||
         (nq && rt_memcpy_h2d(b + oq, m.treelets.data(), nq) != 0)) {

@@ -17,7 +17,8 @@
 //           odd leaf ends with an all-zero triangle), so a small leaf needs no index of its own;
 //           records at other positions are unused;
 //  * tree / ltris  for leaves of at least MIRROR_TREE_LEAF triangles, a leaf tree instead
-//           (leaftree.h): the first record holds po = the root node, pf = 2;
+//           (leaftree.h): the first record holds po = the root node, pf = 2; ltris goes to the
+//           device field-major (rt_ltris_device_layout);
 //  * flat   the leaf trees' flat cluster and cut lists (leaftree.h, cooperative walk);
 //  * treelets  the BVH cut into subtrees of at most 63 nodes for the lone-pixel kernel
 //           (rt_lone.hip): from a root, nodes are taken breadth first while they fit; the nodes of
@@ -56,6 +57,10 @@ struct MirrorHost {
 void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t* face_indices, size_t index_count,
                      const GPUFace* faces, size_t face_count, const GPUVertex* vertices, size_t vertex_count,
                      MirrorHost* out);
+
+// The device copy of MirrorHost::ltris: field-major (record i: A at float4 i, B at n + i, C at
+// 2n + i), so a load instruction of a cluster's 16 lanes touches 2 cache lines instead of 6.
+std::vector<float> rt_ltris_device_layout(const std::vector<float>& ltris);
 
 // The treelets alone (also called by rt_build_mirror).
 void rt_build_treelets(const GPUBVHNode* nodes, size_t node_count, std::vector<float>& out);

@@ -596,7 +596,9 @@ __device__ __forceinline__ void tree_leaf(const float4* tris, const float4* tree
     L.nan = !(h.best == h.best);
     const bool cull_ok = R.fast;
     const f3 rnd = cull_ok ? rtm::mk(1.0f / R.nd.x, 1.0f / R.nd.y, 1.0f / R.nd.z) : rtm::mk(0.0f, 0.0f, 0.0f);
-    const uint32_t end = __float_as_uint(tree[4 * (size_t)root + 3].y);
+    const float4 KR = tree[4 * (size_t)root + 3];
+    const uint32_t end = __float_as_uint(KR.y);
+    const size_t ln = __float_as_uint(KR.x);  // leaf-tree triangles, field-major (leaftree.h)
     uint32_t k = root;
     while (k < end) {
         const float4* kp = tree + 4 * (size_t)k;
@@ -611,7 +613,7 @@ __device__ __forceinline__ void tree_leaf(const float4* tris, const float4* tree
         if (b != 0xffffffffu) {
             const uint32_t n = info >> 8;
             if (STATS) c.ktri += n;
-            for (uint32_t i = b; i < b + n; i++) leaf_candidate(R, ltris[3 * i], ltris[3 * i + 1], ltris[3 * i + 2], L);
+            for (uint32_t i = b; i < b + n; i++) leaf_candidate(R, ltris[i], ltris[ln + i], ltris[2 * ln + i], L);
             k = skip;
         } else {
             k++;
@@ -675,9 +677,13 @@ __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree
         const f3 rnd = bcast3(rnd_l, r);
         const float best = bcast(h.best, r);
         const f4v K2 = ((ConstF4)(tree + 4 * (size_t)root))[2];
-        const uint32_t cb = __float_as_uint(K2.x), kb = __float_as_uint(K2.z), nk = __float_as_uint(K2.w);
-        const float4* cl = flat + 4 * (size_t)cb;
-        const float4* ct = flat + 4 * (size_t)kb;
+        const f4v KR = ((ConstF4)(tree + 4 * (size_t)root))[3];
+        const uint32_t cb = __float_as_uint(K2.x), nc = __float_as_uint(K2.y), kb = __float_as_uint(K2.z),
+                       nk = __float_as_uint(K2.w);
+        const size_t ln = __float_as_uint(KR.x);
+        // field-major lists (leaftree.h): field f of cluster i at cl[f * nc + i], of cut k at ct[f * nk + k]
+        const float4* cl = flat + cb;
+        const float4* ct = flat + kb;
         LeafBest L;
         L.t = best, L.j = 0, L.id = 0, L.bx = 0.0f, L.by = 0.0f, L.found = false;
         L.nan = !(best == best);
@@ -689,9 +695,9 @@ __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree
             uint32_t s0 = 0, s1 = 0;
             float te = 0.0f;
             if (k < nk) {
-                const float4 K0 = ct[4 * k], K1 = ct[4 * k + 1], K3 = ct[4 * k + 3];
+                const float4 K0 = ct[k], K1 = ct[nk + k], K3 = ct[3 * nk + k];
                 s0 = __float_as_uint(K3.y), s1 = __float_as_uint(K3.z);
-                need = !(cull_ok && (__float_as_uint(K3.w) & 1u) && cluster_cull(B, rnd, cbest, K0, K1, ct[4 * k + 2], K3));
+                need = !(cull_ok && (__float_as_uint(K3.w) & 1u) && cluster_cull(B, rnd, cbest, K0, K1, ct[2 * nk + k], K3));
                 if (order) {  // box entry distance along the ray, only to order the subtrees
                     const float tx1 = (K0.x - B.o.x) * rnd.x, tx2 = (K1.x - B.o.x) * rnd.x;
                     const float ty1 = (K0.y - B.o.y) * rnd.y, ty2 = (K1.y - B.o.y) * rnd.y;
@@ -731,10 +737,10 @@ __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree
                 bool need2 = false;
                 uint32_t tb = 0, n = 0;
                 if (has) {
-                    const float4 Q3 = cl[4 * ci + 3];
+                    const float4 Q3 = cl[3 * nc + ci];
                     const uint32_t info = __float_as_uint(Q3.w);
                     tb = __float_as_uint(Q3.z), n = info >> 8;
-                    need2 = !(cull_ok && (info & 1u) && cluster_cull(B, rnd, cbest, cl[4 * ci], cl[4 * ci + 1], cl[4 * ci + 2], Q3));
+                    need2 = !(cull_ok && (info & 1u) && cluster_cull(B, rnd, cbest, cl[ci], cl[nc + ci], cl[2 * nc + ci], Q3));
                 }
                 const unsigned long long mc = __ballot(need2);
                 const uint32_t nsc = (uint32_t)__popcll(mc);
@@ -754,8 +760,8 @@ __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree
                     if (slot < nsc) {
                         const uint32_t w = scratch[slot], my_tb = w & 0x03ffffffu, my_n = (w >> 26) + 1u;
                         if (i < my_n) {
-                            const size_t t3 = 3 * (size_t)(my_tb + i);
-                            leaf_candidate(B, ltris[t3], ltris[t3 + 1], ltris[t3 + 2], L);
+                            const size_t t = (size_t)(my_tb + i);
+                            leaf_candidate(B, ltris[t], ltris[ln + t], ltris[2 * ln + t], L);
                         }
                     }
                 }

@@ -422,7 +422,8 @@ void upload_mirror(ForeignBuild* b) {
         MirrorHost mh;
         rt_build_mirror(nodes, b->bytes[0] / sizeof(GPUBVHNode), fi, b->bytes[1] / 4, faces, b->bytes[2] / sizeof(GPUFace),
                         verts, b->bytes[3] / sizeof(GPUVertex), &mh);
-        const std::vector<float>* parts[7] = {&mh.tris, &mh.pairs, &mh.tree, &mh.ltris, &mh.spairs, &mh.flat, &mh.treelets};
+        const std::vector<float> lt = rt_ltris_device_layout(mh.ltris);
+        const std::vector<float>* parts[7] = {&mh.tris, &mh.pairs, &mh.tree, &lt, &mh.spairs, &mh.flat, &mh.treelets};
         size_t total = 64;
         for (auto* v : parts) total += v->size() * 4;
         hipStream_t st;
