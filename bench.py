@@ -236,7 +236,31 @@ def under_profiler():
 
 
 def _short(name):
-    return name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+    """Kernel name without return type, namespaces and arguments ("render_fast_kernel_w6<30, false, 17>")."""
+    base = name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+    return base.replace("rtk::", "").replace("rtfast::", "")
+
+
+def read_pmc_pass(d):
+    """One rocprofv3 --pmc output directory: {counter: [value per dispatch]} of the production
+    render kernel, its name, and its dispatch durations (s) from the kernel trace.  When the run
+    dispatched more than one render-kernel variant (a probe at the other occupancy), the variant
+    with the most dispatches is the one reported."""
+    per = {}
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(path)):
+            k = _short(row["Kernel_Name"])
+            if k.startswith("render_fast_kernel"):
+                per.setdefault(k, {}).setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+    if not per:
+        return {}, None, []
+    kernel = max(per, key=lambda k: max(len(v) for v in per[k].values()))
+    durations = []
+    for path in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        for row in csv.DictReader(open(path)):
+            if _short(row["Kernel_Name"]) == kernel:
+                durations.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
+    return per[kernel], kernel, durations
 
 
 def pmc_pass(args, out_dir, timeout_s=150):
@@ -267,19 +291,10 @@ def pmc_pass(args, out_dir, timeout_s=150):
         if r.returncode != 0:
             err = [l for l in r.stderr.splitlines() if "Error" in l or "error" in l or "Traceback" in l]
             return None, f"pass {i} exit {r.returncode}: {' | '.join(err[-3:])[-400:]}"
-        vals = {}
-        for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-            for row in csv.DictReader(open(path)):
-                k = _short(row["Kernel_Name"])
-                if not k.startswith("render_fast_kernel"):
-                    continue
-                kernel = k
-                vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+        vals, k, dur = read_pmc_pass(d)
+        kernel = k or kernel
         if i == 0:
-            for path in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
-                for row in csv.DictReader(open(path)):
-                    if _short(row["Kernel_Name"]).startswith("render_fast_kernel"):
-                        durations.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
+            durations = dur
         if not vals:
             return None, f"pass {i}: no render_fast_kernel rows"
         # rows are per dispatch and counter (summed over XCDs by rocprofv3's csv); mean per dispatch

@@ -21,7 +21,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    return name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+    """Kernel name without return type, namespaces and arguments ("render_fast_kernel_w6<30, false, 17>")."""
+    base = name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+    return base.replace("rtk::", "").replace("rtfast::", "")
 
 
 def main():

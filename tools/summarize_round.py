@@ -26,7 +26,9 @@ SYNC = ("hipStreamSynchronize", "hipDeviceSynchronize", "hipMemcpy", "hipEventSy
 
 
 def short(name):
-    return name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+    """Kernel name without return type, namespaces and arguments ("render_fast_kernel_w6<30, false, 17>")."""
+    base = name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+    return base.replace("rtk::", "").replace("rtfast::", "")
 
 
 def bench_line(path):
@@ -37,21 +39,25 @@ def bench_line(path):
 
 
 def pmc_summary(cfg):
+    """Per pass, the counters of the render-kernel variant with the most dispatches (a probe frame
+    at the other occupancy is left out, as bench.read_pmc_pass does)."""
     out = {"config": cfg, "passes": {}}
     for d in sorted(glob.glob(os.path.join(SRC, f"pmc_{cfg}", "pass*"))):
-        vals = collections.defaultdict(list)
-        meta = None
+        vals = collections.defaultdict(lambda: collections.defaultdict(list))
+        meta = {}
         for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(path)):
                 k = short(r["Kernel_Name"])
                 if not k.startswith("render_fast_kernel"):
                     continue
-                vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-                meta = {"kernel": k, "vgpr": int(r["VGPR_Count"]), "sgpr": int(r["SGPR_Count"]),
-                        "lds_bytes": int(r["LDS_Block_Size"]), "scratch_bytes": int(r.get("Scratch_Size", 0) or 0),
-                        "grid": int(r["Grid_Size"])}
-        out["passes"][os.path.basename(d)] = {"kernel": meta, "dispatches": max((len(v) for v in vals.values()), default=0),
-                                             "counters_mean": {c: sum(v) / len(v) for c, v in sorted(vals.items())}}
+                vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                meta[k] = {"kernel": k, "vgpr": int(r["VGPR_Count"]), "sgpr": int(r["SGPR_Count"]),
+                           "lds_bytes": int(r["LDS_Block_Size"]), "scratch_bytes": int(r.get("Scratch_Size", 0) or 0),
+                           "grid": int(r["Grid_Size"])}
+        k = max(vals, key=lambda x: max(len(v) for v in vals[x].values())) if vals else None
+        v = vals[k] if k else {}
+        out["passes"][os.path.basename(d)] = {"kernel": meta.get(k), "dispatches": max((len(x) for x in v.values()), default=0),
+                                             "counters_mean": {c: sum(x) / len(x) for c, x in sorted(v.items())}}
     return out
 
 
@@ -73,6 +79,10 @@ def main():
             s["derived"]["hbm"] = r.get("hbm")
             json.dump(s, open(os.path.join(OUT, f"{a.tag}_{cfg}_pmc.json"), "w"), indent=1)
             print(cfg, "frac", r.get("frac"), "kernel_ms", r.get("kernel_ms"), "lanes", r.get("lane_utilization"))
+        tl = os.path.join(SRC, f"trace_{cfg}.log")
+        if os.path.exists(tl) and bench_line(tl):
+            # the bench line printed by the profiled command itself (PMC pass skipped under a profiler)
+            json.dump(bench_line(tl), open(os.path.join(OUT, f"{a.tag}_{cfg}_trace_bench.json"), "w"), indent=1)
         t = os.path.join(SRC, f"trace_{cfg}", "run_kernel_stats.csv")
         if os.path.exists(t):
             shutil.copy(t, os.path.join(OUT, f"{a.tag}_{cfg}_kernel_stats.csv"))
