@@ -27,6 +27,10 @@ ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 # Numerics flags shared by every translation unit of the product: no FMA contraction, IEEE
 # fp32 division and square root (bit-exact agreement between host code, kernels and oracle).
 FP_FLAGS = ["-ffp-contract=off", "-fno-fast-math"]
+# Device code generation: branches on wave-uniform conditions stay scalar branches instead of being
+# structurized like divergent ones (config 2: 15.65 vs 15.93 ms per frame, three interleaved runs
+# on one box, tools/build_variant.sh + tools/gpu_variants.sh; config 4 unchanged).
+HIP_CODEGEN_FLAGS = ["-mllvm", "-structurizecfg-skip-uniform-regions=1"]
 HOST_SOURCES = ["scene.cpp", "objload.cpp", "mirror.cpp", "leaftree.cpp", "xorwow.cpp", "image.cpp", "shard.cpp"]
 # the render kernel families compile as separate translation units, in parallel (rt_render.h)
 HIP_SOURCES = ["rt_fast_prod.hip", "rt_fast_timing.hip", "rt_fast_ab.hip", "rt_fast_ab2.hip", "rt_fast_refill.hip",
@@ -59,7 +63,7 @@ def build_product(force=False):
     for src in HIP_SOURCES:
         obj = os.path.join(BUILD, src + ".o")
         jobs.append((obj, [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *FP_FLAGS,
-                           "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics", "-fno-slp-vectorize",
+                           "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics", "-fno-slp-vectorize", *HIP_CODEGEN_FLAGS,
                            "-I", INC, "-I", CSRC, "-c", os.path.join(CSRC, src), "-o", obj]))
     for src in HOST_SOURCES:
         obj = os.path.join(BUILD, src + ".o")
