@@ -535,6 +535,8 @@ def run(args):
     def refill(kw):  # the probe (lane_cost) runs without refill
         if "lane_cost" in kw:
             return kw
+        if args.tracer != "fast" and "wave_clock" not in kw and "stats" not in kw:  # counts: production kernel
+            kw = dict(kw, tracer=args.tracer)
         kw = dict(occupancy, **kw)
         return kw if args.foreign else dict(kw, refill_lanes=args.refill)
 
@@ -705,7 +707,7 @@ def run(args):
             "config": {"workload": desc, "scene": scene_name, "width": W, "height": H, "spp": SPP,
                        "bounces": BOUNCES, "parallelism": f"tiles{world}" if sharded else "single",
                        "camera_samples_per_s": round(W * H * SPP * args.steps / elapsed, 1),
-                       "segments_per_step": round(segs_total / args.steps, 1)},
+                       "segments_per_step": round(segs_total / args.steps, 1), "tracer": args.tracer},
             "roofline": roof,
             "rank_kernel_ms": [round(x, 3) for x in rank_kernel_ms],
             "setup_s": round(setup_s, 2),
@@ -804,6 +806,8 @@ def main():
     ap.add_argument("--lane-units", type=float, default=48000.0,
                     help="rt_lane_plan parallel_units (MI355X: 48000 measured best for configs 2 and 3 at N = 2-8)")
     ap.add_argument("--tune", type=lambda s: int(s, 0), default=0, help="diagnostic A/B knobs (0 = production)")
+    ap.add_argument("--tracer", default="fast", choices=["fast", "wavefront"],
+                    help="render path of the timed frames: the production kernel or the wavefront tracer (A/B)")
     ap.add_argument("--foreign", action="store_true",
                     help="render a GPUScene filled outside this library (the reference's Scene::Upload pattern): "
                          "fingerprint-gated mirror, no host synchronisation per frame")

@@ -26,7 +26,7 @@ LIB_PATH = os.path.join(PKG_DIR, "librt_hip.so")
 ASSETS_DIR = os.path.join(ROOT_DIR, "assets")
 
 RT_RENDER_STATS = 1
-TRACERS = {"fast": 0, "ref": 2, "flat": 4}  # rt_render_params.flags
+TRACERS = {"fast": 0, "ref": 2, "flat": 4, "wavefront": 8}  # rt_render_params.flags
 STAT_NAMES = ("segments", "nodes", "tri_tests", "tri_accepts", "sphere_accepts", "hits", "misses", "cycles_tree_cut",
               "wave_small_iters", "lane_small", "wave_big_tris", "lane_big_tris", "wave_segment_iters",
               "lane_segments", "tree_nodes", "tree_tri_tests", "cycles_small", "cycles_big", "cycles_total",

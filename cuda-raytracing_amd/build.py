@@ -34,7 +34,7 @@ HIP_CODEGEN_FLAGS = ["-mllvm", "-structurizecfg-skip-uniform-regions=1"]
 HOST_SOURCES = ["scene.cpp", "objload.cpp", "mirror.cpp", "leaftree.cpp", "xorwow.cpp", "image.cpp", "shard.cpp"]
 # the render kernel families compile as separate translation units, in parallel (rt_render.h)
 HIP_SOURCES = ["rt_fast_prod.hip", "rt_fast_timing.hip", "rt_fast_ab.hip", "rt_fast_ab2.hip", "rt_fast_refill.hip",
-               "rt_fast_stats.hip", "rt_ref.hip", "rt_lone.hip", "rt_kernel.hip", "image.hip", "bvh_build.hip", "comm.hip"]
+               "rt_fast_stats.hip", "rt_ref.hip", "rt_lone.hip", "rt_wavefront.hip", "rt_kernel.hip", "image.hip", "bvh_build.hip", "comm.hip"]
 
 
 def _run(cmd):

@@ -706,6 +706,11 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     if ((p->lane_slots || p->lane_cost || p->refill_lanes) && (gate || !a.tris || want_flat))
         return set_error("rt_render: lane_slots / lane_cost / refill_lanes need the production tracer on an rt_scene_upload scene");
     if (p->lane_cost && p->refill_lanes) return set_error("rt_render: lane_cost probes run without refill");
+    const bool want_wf = (p->flags & RT_RENDER_TRACER_WAVEFRONT) != 0;
+    if (want_wf && (gate || !a.tris || want_flat || stats || p->lane_cost || p->refill_lanes || p->wave_clock ||
+                    p->lone_count))
+        return set_error("rt_render: the wavefront tracer needs an rt_scene_upload scene and no statistics / lane_cost / "
+                         "wave_clock / refill / lone frames");
     const bool lone = p->lone_count > 0;
     if (p->lone_count < 0 || p->lone_count > (int64_t)1 << 28 || (lone && !p->lone_slots))
         return set_error("rt_render: lone_count must be in [0, 2^28] with lone_slots");
@@ -734,6 +739,8 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
         e = launch_ref_tracer(false, a, tiles * 4, depth, stats, s);
     else if (want_flat)
         e = launch_ref_tracer(true, a, tiles * 4, depth, stats, s);
+    else if (want_wf)
+        e = launch_wavefront(a, depth, s);
     else if (lone) {
         // the lone-pixel kernel on a side stream forked from and joined back into the caller's
         LoneStreams* ls = lone_streams(s);

@@ -20,4 +20,7 @@ hipError_t launch_lone(const RenderArgs& a, const int32_t* lone_slots, int lone_
 // The reference-layout tracer (flat = false) or the exact-division flat tracer (rt_ref.hip).
 hipError_t launch_ref_tracer(bool flat, const RenderArgs& a, int waves, int depth, bool stats, hipStream_t s);
 
+// The wavefront tracer (rt_wavefront.hip): shade / trace launches per segment generation.
+hipError_t launch_wavefront(const RenderArgs& a, int depth, hipStream_t s);
+
 }  // namespace rtk

@@ -218,6 +218,11 @@ typedef struct rt_render_params {
 #define RT_RENDER_STATS 1          /* count traversal work (slower kernel variant) */
 #define RT_RENDER_TRACER_REF 2     /* force the reference-layout tracer (A/B, tests) */
 #define RT_RENDER_TRACER_FLAT 4    /* force the exact-division flat tracer (A/B, tests) */
+#define RT_RENDER_TRACER_WAVEFRONT 8 /* wavefront tracer: a shade launch and a persistent trace launch
+                                        per segment generation, rays refilled lane by lane (same
+                                        results; rt_scene_upload scenes, no statistics / lane_cost /
+                                        wave_clock / refill / lone frames; one frame at a time per
+                                        device) */
 
 enum {
     RT_STAT_SEGMENTS = 0,   /* GetRayHit calls */

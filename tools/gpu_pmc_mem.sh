@@ -24,16 +24,17 @@ while read -r line; do
 done < "$GROUPS_FILE"
 cd "$R"
 python3 - <<'PY'
-import csv, glob, collections, json
+import csv, glob, collections, json, os
 acc = collections.defaultdict(float); n = collections.Counter()
 for p in glob.glob("gpurun_out/pmc_mem/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(p)):
         k = r["Kernel_Name"]
-        if "render_fast_kernel" not in k or "false" not in k: continue
+        if not any(f in k for f in os.environ.get("KFILTER", "render_fast_kernel").split(",")): continue
+        if "render_fast_kernel" in k and "false" not in k: continue
         key = (k.split("(")[0].replace("void rtk::", ""), r["Counter_Name"])
         acc[key] += float(r["Counter_Value"]); n[key] += 1
 out = collections.defaultdict(dict)
 for (k, c), v in sorted(acc.items()):
-    out[k][c] = v / n[(k, c)]
+    out[k][c] = v if os.environ.get("SUM") else v / n[(k, c)]
 print(json.dumps(out, indent=1))
 PY
