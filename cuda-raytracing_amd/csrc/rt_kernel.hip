@@ -711,6 +711,9 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
                     p->lone_count))
         return set_error("rt_render: the wavefront tracer needs an rt_scene_upload scene and no statistics / lane_cost / "
                          "wave_clock / refill / lone frames");
+    // its pixel state packs the sample count in 16 bits and the bounce in 8; a generation per segment
+    if (want_wf && (p->spp > 65535 || p->bounces > 255 || (int64_t)p->spp * p->bounces > 65536))
+        return set_error("rt_render: the wavefront tracer needs spp <= 65535, bounces <= 255, spp x bounces <= 65536");
     const bool lone = p->lone_count > 0;
     if (p->lone_count < 0 || p->lone_count > (int64_t)1 << 28 || (lone && !p->lone_slots))
         return set_error("rt_render: lone_count must be in [0, 2^28] with lone_slots");

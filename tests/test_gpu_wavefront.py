@@ -109,3 +109,5 @@ def test_wavefront_misuse_is_refused(rt):
     st = torch.zeros(24, dtype=torch.int64, device="cuda")
     with pytest.raises(RuntimeError, match="wavefront"):
         rt.render(s, out, out, w, h, 1, 1, 0, stats=st, tracer="wavefront")
+    with pytest.raises(RuntimeError, match="spp x bounces"):
+        rt.render(s, out, out, w, h, 300, 300, 0, tracer="wavefront")
