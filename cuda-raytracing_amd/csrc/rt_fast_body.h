@@ -363,8 +363,11 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(5))) void 
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
     render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds + threadIdx.x, ovf}, scratch_lds);
 }
+#ifndef RT_W6_WAVES
+#define RT_W6_WAVES 6  // experiments: tools/build_variant.sh NAME -DRT_W6_WAVES=7
+#endif
 template <int STACK, bool STATS, int MODE>
-__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(6))) void render_fast_kernel_w6(RenderArgs a) {
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(RT_W6_WAVES))) void render_fast_kernel_w6(RenderArgs a) {
     constexpr int SL = STACK < 16 ? STACK : 16;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
     __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
     __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
