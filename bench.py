@@ -549,13 +549,13 @@ def run(args):
         setup_s += time.perf_counter() - t1
         plan_info = dict(plan_info or {}, lanes=lane_info)
 
-    # occupancy (rt_render_params.waves_per_simd): time one untimed frame at 5 and at 6 waves per
-    # SIMD (twice each, on a copy of the RNG states) and keep the faster
+    # occupancy (rt_render_params.waves_per_simd): time one untimed frame at 5, 6 and 7 waves per
+    # SIMD (twice each, on a copy of the RNG states) and keep the fastest
     if args.occupancy == "auto" and not args.pmc_child:
         t1 = time.perf_counter()
         rng_saved = rng.clone()
         best = {}
-        for wps in (5, 6, 5, 6):
+        for wps in (5, 6, 7, 5, 6, 7):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             render(0, bufs[0], None, waves_per_simd=wps)
@@ -567,9 +567,9 @@ def run(args):
         if world > 1:
             # one variant for the whole job: every rank takes the setting whose slowest rank is fastest
             cdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
-            t = torch.tensor([best[5], best[6]], dtype=torch.float64, device=cdev)
+            t = torch.tensor([best[5], best[6], best[7]], dtype=torch.float64, device=cdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            best = {5: float(t[0]), 6: float(t[1])}
+            best = {5: float(t[0]), 6: float(t[1]), 7: float(t[2])}
         occupancy["waves_per_simd"] = min(best, key=best.get)
         setup_s += time.perf_counter() - t1
         plan_info = dict(plan_info or {}, occupancy={"waves_per_simd": occupancy["waves_per_simd"],
@@ -799,7 +799,7 @@ def main():
                          "longest-processing-time deal over ranks) or round-robin in row-major order")
     ap.add_argument("--refill", type=int, default=0,
                     help="rt_render refill_lanes: a wave refills this many idle lanes from the frame's queue (0 = off)")
-    ap.add_argument("--occupancy", default="auto", choices=["auto", "5", "6"],
+    ap.add_argument("--occupancy", default="auto", choices=["auto", "5", "6", "7"],
                     help="rt_render waves_per_simd; auto = time one untimed frame at each and keep the faster")
     ap.add_argument("--lanes", default="auto", choices=["auto", "on", "off"],
                     help="lane plan (rt_lane_plan: split the waves of the frame's costliest pixels); auto = on for N > 1")

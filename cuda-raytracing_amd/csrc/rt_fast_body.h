@@ -344,9 +344,9 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
     }
 }
 
-// The production kernel.  The _w5 / _w6 variants ask the compiler for 5 / 6 waves per SIMD
-// (fewer registers, some spilled) -- an occupancy / spill trade-off (RT_TUNE bits 9-10:
-// 0 = _w5, the default; 1 = unconstrained; 2 = _w6).
+// The production kernel.  The _w5 / _w6 / _w7 variants ask the compiler for 5 / 6 / 7 waves per
+// SIMD (fewer registers, more spilled) -- an occupancy / spill trade-off (RT_TUNE bits 9-10:
+// 0 = _w5, the default; 1 = unconstrained; 2 = _w6; 3 = _w7).
 template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
     constexpr int SL = STACK < 16 ? STACK : 16;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
@@ -363,11 +363,16 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(5))) void 
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
     render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds + threadIdx.x, ovf}, scratch_lds);
 }
-#ifndef RT_W6_WAVES
-#define RT_W6_WAVES 6  // experiments: tools/build_variant.sh NAME -DRT_W6_WAVES=7
-#endif
 template <int STACK, bool STATS, int MODE>
-__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(RT_W6_WAVES))) void render_fast_kernel_w6(RenderArgs a) {
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(6))) void render_fast_kernel_w6(RenderArgs a) {
+    constexpr int SL = STACK < 16 ? STACK : 16;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
+    __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
+    __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
+    uint32_t ovf[STACK > SL ? STACK - SL : 1];
+    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds + threadIdx.x, ovf}, scratch_lds);
+}
+template <int STACK, bool STATS, int MODE>
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(7))) void render_fast_kernel_w7(RenderArgs a) {
     constexpr int SL = STACK < 16 ? STACK : 16;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
     __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
     __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
@@ -409,9 +414,8 @@ hipError_t launch_grid(K kernel, const RenderArgs& args, int waves, bool refill,
 }
 
 // One (STACK, STATS, MODE) variant at the occupancy rt_render_params asks for: statistics frames run
-// the unconstrained kernel; the others 5 waves per SIMD (default) or 6 (waves_per_simd = 6, or
-// RT_TUNE bits 9-10 = 2).  rt_render rejects the retired RT_TUNE overrides 1 (compiler's choice) and
-// 3 (7 waves per SIMD: slower everywhere).
+// the unconstrained kernel; the others 5 waves per SIMD (default), 6 or 7 (waves_per_simd, or
+// RT_TUNE bits 9-10 = 2 / 3).  rt_render rejects the retired RT_TUNE override 1 (compiler's choice).
 template <int STACK, bool STATS, int MODE>
 hipError_t launch_occ(const RenderArgs& args, int waves, hipStream_t stream) {
     constexpr bool refill = (MODE & 64) != 0;  // only these variants drain a refill queue
@@ -419,9 +423,10 @@ hipError_t launch_occ(const RenderArgs& args, int waves, hipStream_t stream) {
         return launch_grid(render_fast_kernel<STACK, true, MODE>, args, waves, refill, stream);
     } else {
         const uint32_t t = (args.tune >> 9) & 3u;
-        const bool w6 = t == 2u || (t == 0u && args.waves_per_simd == 6);
-        return w6 ? launch_grid(render_fast_kernel_w6<STACK, false, MODE>, args, waves, refill, stream)
-                  : launch_grid(render_fast_kernel_w5<STACK, false, MODE>, args, waves, refill, stream);
+        const int w = t == 2u ? 6 : t == 3u ? 7 : args.waves_per_simd;
+        if (w == 7) return launch_grid(render_fast_kernel_w7<STACK, false, MODE>, args, waves, refill, stream);
+        return w == 6 ? launch_grid(render_fast_kernel_w6<STACK, false, MODE>, args, waves, refill, stream)
+                      : launch_grid(render_fast_kernel_w5<STACK, false, MODE>, args, waves, refill, stream);
     }
 }
 
