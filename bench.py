@@ -550,12 +550,15 @@ def run(args):
         plan_info = dict(plan_info or {}, lanes=lane_info)
 
     # occupancy (rt_render_params.waves_per_simd): time one untimed frame at 5, 6 and 7 waves per
-    # SIMD (twice each, on a copy of the RNG states) and keep the fastest
+    # SIMD (twice each, on a copy of the RNG states) and keep the fastest; a strong-scaled shard
+    # (N > 1) also tries the 5-wave build capped at 3 and 4 resident waves per SIMD (dynamic LDS):
+    # config 2 at N = 8, 6.36 ms at 4 vs 6.66 ms at 6 (profiles/r03e_capped_shards.jsonl)
     if args.occupancy == "auto" and not args.pmc_child:
         t1 = time.perf_counter()
         rng_saved = rng.clone()
         best = {}
-        for wps in (5, 6, 7, 5, 6, 7):
+        cands = (5, 6, 7) if world == 1 else (3, 4, 5, 6, 7)
+        for wps in cands + cands:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             render(0, bufs[0], None, waves_per_simd=wps)
@@ -567,9 +570,9 @@ def run(args):
         if world > 1:
             # one variant for the whole job: every rank takes the setting whose slowest rank is fastest
             cdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
-            t = torch.tensor([best[5], best[6], best[7]], dtype=torch.float64, device=cdev)
+            t = torch.tensor([best[w] for w in cands], dtype=torch.float64, device=cdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            best = {5: float(t[0]), 6: float(t[1]), 7: float(t[2])}
+            best = {w: float(x) for w, x in zip(cands, t.tolist())}
         occupancy["waves_per_simd"] = min(best, key=best.get)
         setup_s += time.perf_counter() - t1
         plan_info = dict(plan_info or {}, occupancy={"waves_per_simd": occupancy["waves_per_simd"],
@@ -799,8 +802,9 @@ def main():
                          "longest-processing-time deal over ranks) or round-robin in row-major order")
     ap.add_argument("--refill", type=int, default=0,
                     help="rt_render refill_lanes: a wave refills this many idle lanes from the frame's queue (0 = off)")
-    ap.add_argument("--occupancy", default="auto", choices=["auto", "5", "6", "7"],
-                    help="rt_render waves_per_simd; auto = time one untimed frame at each and keep the faster")
+    ap.add_argument("--occupancy", default="auto", choices=["auto", "1", "2", "3", "4", "5", "6", "7"],
+                    help="rt_render waves_per_simd (1-4: the 5-wave build capped at that residency by dynamic LDS); "
+                         "auto = time one untimed frame at 5 / 6 / 7 (N > 1: also 3 / 4) and keep the fastest")
     ap.add_argument("--lanes", default="auto", choices=["auto", "on", "off"],
                     help="lane plan (rt_lane_plan: split the waves of the frame's costliest pixels); auto = on for N > 1")
     ap.add_argument("--lane-units", type=float, default=48000.0,

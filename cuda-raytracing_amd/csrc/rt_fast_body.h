@@ -402,14 +402,26 @@ int resident_waves(K kernel) {
     return cache[key] = std::max(1, std::min(vgpr_waves, lds_waves)) * 4 * std::max(cus, 1);
 }
 
+// Dynamic LDS that caps `kernel` at `cap` (1-4) resident waves per SIMD: each wave then holds
+// 160 KB / (4 cap) of its CU's LDS (rounded down to 1 KB), so 4 cap waves fit a CU and one more
+// does not.  0 when uncapped.
 template <class K>
-hipError_t launch_grid(K kernel, const RenderArgs& args, int waves, bool refill, hipStream_t stream) {
+size_t cap_lds_bytes(K kernel, int cap) {
+    if (cap < 1 || cap > 4) return 0;
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, (const void*)kernel) != hipSuccess) return 0;
+    const size_t per_wave = (size_t)(160 * 1024 / (4 * cap)) & ~(size_t)1023;
+    return per_wave > fa.sharedSizeBytes ? per_wave - fa.sharedSizeBytes : 0;
+}
+
+template <class K>
+hipError_t launch_grid(K kernel, const RenderArgs& args, int waves, bool refill, hipStream_t stream, size_t lds = 0) {
     int grid = waves;
     if (refill && args.queue_head) {  // refill variants: one grid of resident waves, the rest through the queue
         const int res = resident_waves(kernel);
         if (res > 0) grid = std::min(waves, res);
     }
-    hipLaunchKernelGGL(kernel, dim3(grid), dim3(WAVE), 0, stream, args);
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(WAVE), lds, stream, args);
     return hipGetLastError();
 }
 
@@ -424,6 +436,10 @@ hipError_t launch_occ(const RenderArgs& args, int waves, hipStream_t stream) {
     } else {
         const uint32_t t = (args.tune >> 9) & 3u;
         const int w = t == 2u ? 6 : t == 3u ? 7 : args.waves_per_simd;
+        if (w >= 1 && w <= 4) {  // the 5-wave build, residency capped by dynamic LDS
+            const auto k = render_fast_kernel_w5<STACK, false, MODE>;
+            return launch_grid(k, args, waves, refill, stream, cap_lds_bytes(k, w));
+        }
         if (w == 7) return launch_grid(render_fast_kernel_w7<STACK, false, MODE>, args, waves, refill, stream);
         return w == 6 ? launch_grid(render_fast_kernel_w6<STACK, false, MODE>, args, waves, refill, stream)
                       : launch_grid(render_fast_kernel_w5<STACK, false, MODE>, args, waves, refill, stream);

@@ -653,8 +653,8 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     const int waves = p->lane_slots ? (int)(p->lane_slot_count / WAVE) : tiles * 4;  // production tracer's grid
     a.entry_count = (long long)waves * WAVE;
     if (p->refill_lanes < 0 || p->refill_lanes > 64) return set_error("rt_render: refill_lanes must be in [0, 64]");
-    if (p->waves_per_simd != 0 && (p->waves_per_simd < 5 || p->waves_per_simd > 7))
-        return set_error("rt_render: waves_per_simd must be 0, 5, 6 or 7");
+    if (p->waves_per_simd < 0 || p->waves_per_simd > 7)
+        return set_error("rt_render: waves_per_simd must be 0 (default), 1-4 (LDS-capped residency), 5, 6 or 7");
     if (((p->tune >> 9) & 3u) == 1u)
         return set_error("rt_render: RT_TUNE occupancy override 1 (compiler's choice) is not built");
     a.waves_per_simd = p->waves_per_simd;

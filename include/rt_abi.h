@@ -198,8 +198,10 @@ typedef struct rt_render_params {
     /* Occupancy of the production tracer: 0 = the default (5 waves per SIMD, 96 registers);
      * 6 = 6 waves per SIMD (80 registers, more spills), 7 = 7 (72 registers) -- faster on some
      * scenes (config 2: 16.2 / 15.3 vs 16.9 ms), slower on others (config 4: 95 vs 90 ms at 6);
-     * bench.py picks it per configuration by timing one untimed probe frame of each.  Any other
-     * value is an error. */
+     * bench.py picks it per configuration by timing one untimed probe frame of each.  1-4 = the
+     * 5-wave build with its residency capped at that many waves per SIMD by dynamic LDS (each
+     * wave reserves 160 KB / (4 x cap) of its CU's LDS): fewer co-resident waves for the
+     * latency-bound long waves of a strong-scaled shard.  Any other value is an error. */
     int32_t waves_per_simd;
     /* Lone pixels (production tracer; rt_lone.hip): DEVICE int32 slots (the lane_slots numbering)
      * that the lone-pixel kernel renders one per wave -- all 64 lanes on the pixel's one ray, the BVH

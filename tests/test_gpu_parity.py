@@ -346,9 +346,10 @@ def test_full_size_tiles(rt, cfg, which, w, h, spp, picks):
 @pytest.mark.parametrize("which,plane_n", [("bunny", None), ("bunny4", None)])
 def test_occupancy_variants_agree(rt, which, plane_n):
     """The production kernel at 5, 6 and 7 waves per SIMD (rt_render_params.waves_per_simd: the
-    compiler spills differently, the arithmetic is the same) renders identical frames and states."""
+    compiler spills differently, the arithmetic is the same) and the 5-wave build with its residency
+    capped at 2 waves per SIMD by dynamic LDS render identical frames and states."""
     w, h, res = 256, 144, {}
-    for wps in (5, 6, 7):
+    for wps in (5, 6, 7, 2):
         s = make_scene(rt, which, w, h, plane_n)
         rng = rt.alloc_rng(w * h)
         rt.init_rng_states(rng, w, h, T.SEED)
@@ -357,5 +358,5 @@ def test_occupancy_variants_agree(rt, which, plane_n):
         rt.render(s, out, last, w, h, 4, 6, 0, waves_per_simd=wps)
         torch.cuda.synchronize()
         res[wps] = (rt.surface_view(out, w).cpu().numpy().copy(), rng.view(-1, 12)[:, :6].cpu().numpy().copy())
-    for wps in (6, 7):
+    for wps in (6, 7, 2):
         assert np.array_equal(res[5][0], res[wps][0]) and np.array_equal(res[5][1], res[wps][1]), wps
