@@ -433,23 +433,72 @@ def make_plan(rt, scene, W, H, SPP, BOUNCES, rank, world, plan_kind, dev):
                            "invalid_wave_clocks": nbad}
 
 
-def make_lane_map(rt, render, rng, slots, units, dev):
+def make_lane_map(rt, render, rng, slots, units, dev, refine=0, theta=0.75):
     """rt_lane_plan for this rank's list: one probe frame of per-pixel work (timing variant of the
-    production kernel, set-up, untimed) on a copy of the RNG states, then the split plan.
-    Returns (device int32 lane map, info)."""
+    production kernel, set-up, untimed) on a copy of the RNG states, then the split plan, then up to
+    `refine` rounds of measured refinement (refine_lane_map).  Returns (device int32 lane map, info)."""
     import torch
 
     rng_saved = rng.clone()
     cost = torch.zeros(slots, dtype=torch.int32, device=dev)  # one per slot of the tile list
     t0 = time.perf_counter()
-    render(cost)
+    render(lane_cost=cost)
     torch.cuda.synchronize()
     probe_s = time.perf_counter() - t0
     rng.copy_(rng_saved)
     del rng_saved
-    lm, nlong = rt.lane_plan(cost.cpu().numpy(), units, 1.0)
-    return torch.from_numpy(lm).to(dev), {"lane_probe_s": round(probe_s, 4), "waves": int(lm.size // 64),
-                                          "long_waves": nlong, "parallel_units": units}
+    cost_np = cost.cpu().numpy()
+    lm, nlong = rt.lane_plan(cost_np, units, 1.0)
+    info = {"lane_probe_s": round(probe_s, 4), "waves": int(lm.size // 64), "long_waves": nlong, "parallel_units": units}
+    if refine > 0:
+        lm, info["refine"] = refine_lane_map(rt, render, rng, lm, cost_np, refine, theta, dev)
+        info["waves"] = int(lm.size // 64)
+    return torch.from_numpy(lm).to(dev), info
+
+
+def refine_lane_map(rt, render, rng, lm, cost, rounds, theta, dev, waves_per_simd=6):
+    """Measured lane-plan refinement (rt_lane_refine): time a frame of the map (production kernel, HIP
+    events, best of two, on a copy of the RNG states), take one timing frame's per-wave clocks, split
+    the waves within `theta` of the longest, and keep the new map only while the frame gets faster.
+    Config 2 at N = 8, shard by shard: 5.93 -> 4.56 ms in one round (profiles/r03e_lane_refine.jsonl).
+    Every candidate is a permutation of the shard's slots, so the frame is the same bit for bit."""
+    import torch
+
+    saved = rng.clone()
+
+    def timed(m_dev):
+        best = 1e30
+        for _ in range(2):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            render(lane_slots=m_dev, waves_per_simd=waves_per_simd)
+            e1.record()
+            torch.cuda.synchronize()
+            rng.copy_(saved)
+            best = min(best, e0.elapsed_time(e1))
+        return best
+
+    def clocks(m_dev):
+        clk = torch.zeros(m_dev.numel() // 64, dtype=torch.int64, device=dev)
+        render(lane_slots=m_dev, wave_clock=clk)
+        torch.cuda.synchronize()
+        rng.copy_(saved)
+        return sanitize_wave_clocks(clk.cpu().numpy())[0]
+
+    t0 = time.perf_counter()
+    cur, cur_dev = lm, torch.from_numpy(lm).to(dev)
+    best_ms = timed(cur_dev)
+    hist, kept = [round(best_ms, 3)], 0
+    for _ in range(rounds):
+        new, nsplit = rt.lane_refine(cur, cost, clocks(cur_dev), theta)
+        new_dev = torch.from_numpy(new).to(dev)
+        ms = timed(new_dev)
+        hist.append(round(ms, 3))
+        if not nsplit or ms >= best_ms:
+            break
+        cur, cur_dev, best_ms, kept = new, new_dev, ms, kept + 1
+    del saved
+    return cur, {"theta": theta, "frame_ms": hist, "rounds_kept": kept, "s": round(time.perf_counter() - t0, 3)}
 
 
 def run(args):
@@ -523,12 +572,13 @@ def run(args):
     lane_slots = None
 
     def render(i, cur, prev, **kw):
+        ls = kw.pop("lane_slots", lane_slots)
         if sharded:
             rt.render(scene, None, prev, W, H, SPP, BOUNCES, i, rank, world, out_shard=cur, tile_list=tile_list,
-                      tune=args.tune, lane_slots=lane_slots, **refill(kw))
+                      tune=args.tune, lane_slots=ls, **refill(kw))
         else:
             rt.render(target, cur, prev, W, H, SPP, BOUNCES, i, tile_list=tile_list, tune=args.tune,
-                      lane_slots=lane_slots, **refill(kw))
+                      lane_slots=ls, **refill(kw))
 
     occupancy = {"waves_per_simd": 0 if args.occupancy == "auto" else int(args.occupancy)}
 
@@ -544,8 +594,9 @@ def run(args):
     lanes_on = args.lanes == "on" or (args.lanes == "auto" and sharded)
     if lanes_on and not args.foreign and tile_list is not None:
         t1 = time.perf_counter()
-        lane_slots, lane_info = make_lane_map(rt, lambda cost: render(0, bufs[0], None, lane_cost=cost), rng,
-                                              tile_list.numel() * 256, args.lane_units, dev)
+        lane_slots, lane_info = make_lane_map(rt, lambda **kw: render(0, bufs[0], None, **kw), rng,
+                                              tile_list.numel() * 256, args.lane_units, dev,
+                                              refine=args.lane_refine if sharded else 0, theta=args.lane_theta)
         setup_s += time.perf_counter() - t1
         plan_info = dict(plan_info or {}, lanes=lane_info)
 
@@ -807,6 +858,10 @@ def main():
                          "auto = time one untimed frame at 5 / 6 / 7 (N > 1: also 3 / 4) and keep the fastest")
     ap.add_argument("--lanes", default="auto", choices=["auto", "on", "off"],
                     help="lane plan (rt_lane_plan: split the waves of the frame's costliest pixels); auto = on for N > 1")
+    ap.add_argument("--lane-refine", type=int, default=3,
+                    help="N > 1: rounds of measured lane-plan refinement (rt_lane_refine; 0 = the model's plan only)")
+    ap.add_argument("--lane-theta", type=float, default=0.75,
+                    help="rt_lane_refine theta: waves measured within this fraction of the longest are split")
     ap.add_argument("--lane-units", type=float, default=48000.0,
                     help="rt_lane_plan parallel_units (MI355X: 48000 measured best for configs 2 and 3 at N = 2-8)")
     ap.add_argument("--tune", type=lambda s: int(s, 0), default=0, help="diagnostic A/B knobs (0 = production)")

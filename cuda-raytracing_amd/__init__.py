@@ -98,6 +98,8 @@ SIGNATURES = {
     "rt_lane_plan_capacity": (ctypes.c_int64, [ctypes.c_int64]),
     "rt_lane_plan": (ctypes.c_int64, [_P, ctypes.c_int64, ctypes.c_double, ctypes.c_double, _P, ctypes.c_int64, _P]),
     "rt_lone_plan": (ctypes.c_int64, [_P, ctypes.c_int64, ctypes.c_int64, _U32, _P]),
+    "rt_lane_refine": (ctypes.c_int64, [_P, ctypes.c_int64, _P, ctypes.c_int64, _P, ctypes.c_double, _P, ctypes.c_int64,
+                                        _P]),
     "rt_init_rng_tiles": (_I, [_P, _I, _I, _P, ctypes.c_int64, _U32, _P]),
     "rt_unshard_tiles": (_I, [_P, _U64, _I, _I, _I, _P, ctypes.c_int64, _P, _P]),
     "rt_comm_unique_id": (_I, [_P]),
@@ -463,6 +465,23 @@ def lane_plan(cost, parallel_units=48000.0, slack=1.0):
     if n < 0:
         raise RTError("rt_lane_plan failed: " + lib().rt_last_error().decode(errors="replace"))
     return out[:n].copy(), int(nlong.value)
+
+
+def lane_refine(lane_map, cost, wave_ticks, theta=0.75):
+    """rt_lane_refine: (int32 numpy lane map, waves made by splitting) -- the waves of `lane_map`
+    whose measured clock (numpy int64 [waves], a timing frame's wave_clock) is within theta of the
+    longest split in two, all waves ordered longest first."""
+    m = np.ascontiguousarray(np.asarray(lane_map, dtype=np.int32).ravel())
+    cost = np.ascontiguousarray(np.asarray(cost).astype(np.uint32))
+    ticks = np.ascontiguousarray(np.asarray(wave_ticks, dtype=np.int64))
+    assert m.size % 64 == 0 and ticks.size >= m.size // 64
+    out = np.empty(2 * m.size, dtype=np.int32)
+    nsplit = ctypes.c_int64(0)
+    n = int(lib().rt_lane_refine(m.ctypes.data, m.size, cost.ctypes.data, cost.size, ticks.ctypes.data, float(theta),
+                                 out.ctypes.data, out.size, ctypes.byref(nsplit)))
+    if n < 0:
+        raise RTError("rt_lane_refine failed: " + lib().rt_last_error().decode(errors="replace"))
+    return out[:n].copy(), int(nsplit.value)
 
 
 def lone_plan(cost, max_lone, min_cost=1):

@@ -199,6 +199,81 @@ extern "C" int64_t rt_lane_plan(const uint32_t* cost, int64_t slots, double para
     return n;
 }
 
+// Measured refinement of a lane map.  The model above prices a wave from its pixels' probe work;
+// on the device, multi-pixel waves at the target take about twice as long as the single costliest
+// pixel (which runs its DFS with the whole wave, rt_fast.h lone_traverse), so at N = 8 the plan's
+// long waves are each rank's frame.  Here the waves a timing frame of the map itself MEASURED
+// within `theta` of the longest (wave_ticks: rt_render_params.wave_clock) are split in two -- their
+// pixels in decreasing probe work dealt alternately, so each half keeps every other of the
+// costliest -- and all waves are ordered by expected duration, longest first (a half at 3/4 of its
+// parent's clock).  The caller times the new map and keeps it only if the frame got faster
+// (bench.py refine_lane_map).  A lane map is a permutation of the shard's slots, so any refinement
+// renders the same pixels bit for bit.
+extern "C" int64_t rt_lane_refine(const int32_t* lane_slots, int64_t entries, const uint32_t* cost, int64_t slots,
+                                  const int64_t* wave_ticks, double theta, int32_t* out, int64_t capacity,
+                                  int64_t* split_waves) {
+    if (!lane_slots || !cost || !wave_ticks || !out || entries <= 0 || entries % 64 != 0 || slots <= 0 ||
+        slots > ((int64_t)1 << 30) || entries > ((int64_t)1 << 32) || capacity < 2 * entries || !(theta > 0) ||
+        !(theta <= 1)) {
+        rt_internal_set_error("rt_lane_refine: bad arguments (entries a positive multiple of 64, capacity >= 2 * entries, "
+                              "0 < theta <= 1)");
+        return -1;
+    }
+    const int64_t nw = entries / 64;
+    int64_t longest = 0;
+    for (int64_t w = 0; w < nw; w++) {
+        if (wave_ticks[w] < 0) {
+            rt_internal_set_error("rt_lane_refine: negative wave clock");
+            return -1;
+        }
+        longest = std::max(longest, wave_ticks[w]);
+    }
+    for (int64_t i = 0; i < entries; i++)
+        if (lane_slots[i] < -1 || lane_slots[i] >= slots) {
+            rt_internal_set_error("rt_lane_refine: lane map entry outside [-1, slots)");
+            return -1;
+        }
+    const double cut = theta * (double)longest;
+    struct Wave {
+        std::vector<int32_t> lanes;
+        double est;
+    };
+    std::vector<Wave> waves;
+    waves.reserve(2 * nw);
+    int64_t nsplit = 0;
+    for (int64_t w = 0; w < nw; w++) {
+        Wave v;
+        for (int l = 0; l < 64; l++)
+            if (lane_slots[w * 64 + l] >= 0) v.lanes.push_back(lane_slots[w * 64 + l]);
+        if (v.lanes.empty()) continue;
+        v.est = (double)wave_ticks[w];
+        if (longest > 0 && v.est >= cut && v.lanes.size() > 1) {
+            std::vector<int32_t> by = v.lanes;
+            std::stable_sort(by.begin(), by.end(), [&](int32_t a, int32_t b) { return cost[a] > cost[b]; });
+            Wave h[2];
+            for (size_t i = 0; i < by.size(); i++) h[i & 1].lanes.push_back(by[i]);
+            for (Wave& x : h) {
+                x.est = 0.75 * v.est;
+                waves.push_back(std::move(x));
+            }
+            nsplit += 2;
+        } else {
+            waves.push_back(std::move(v));
+        }
+    }
+    std::vector<int64_t> idx(waves.size());
+    std::iota(idx.begin(), idx.end(), 0);
+    std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return waves[a].est > waves[b].est; });
+    int64_t n = 0;
+    for (int64_t i : idx) {
+        const Wave& v = waves[i];
+        for (int l = 0; l < 64; l++) out[n + l] = l < (int)v.lanes.size() ? v.lanes[l] : -1;
+        n += 64;
+    }
+    if (split_waves) *split_waves = nsplit;
+    return n;
+}
+
 // Lone-pixel plans (rt_render_params.lone_slots, rt_lone.hip): the costliest pixels of the probe
 // frame, each to be rendered by a wave of its own, are taken out of the lane plan.
 extern "C" int64_t rt_lone_plan(uint32_t* cost, int64_t slots, int64_t max_lone, uint32_t min_cost, int32_t* lone_slots) {

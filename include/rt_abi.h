@@ -312,6 +312,16 @@ int64_t rt_lane_plan_capacity(int64_t slots);
  * priority_waves).  Returns the entries written (a multiple of 64), or -1 on bad arguments. */
 int64_t rt_lane_plan(const uint32_t* cost, int64_t slots, double parallel_units, double slack,
                      int32_t* lane_slots, int64_t capacity, int64_t* long_waves);
+/* Measured refinement of a HOST lane map of `entries` entries over `slots` slots: with wave_ticks
+ * [entries / 64] the per-wave clocks of a timing frame of that map (rt_render_params.wave_clock),
+ * every wave of more than one pixel whose clock is at least theta (0 < theta <= 1) x the longest is
+ * split in two (its pixels in decreasing `cost` dealt alternately), and all waves are written to
+ * HOST `out` (capacity >= 2 * entries) ordered by expected duration, longest first.  A map is a
+ * permutation of the slots, so the frame is bit-identical; the caller keeps the refined map only if
+ * a timed frame of it is faster (bench.py refine_lane_map).  *split_waves (optional) receives the
+ * number of waves made by splitting.  Returns the entries written, or -1 on bad arguments. */
+int64_t rt_lane_refine(const int32_t* lane_slots, int64_t entries, const uint32_t* cost, int64_t slots,
+                       const int64_t* wave_ticks, double theta, int32_t* out, int64_t capacity, int64_t* split_waves);
 /* Lone-pixel plans: write to HOST lone_slots (up to max_lone entries) the slots whose probe work
  * `cost` is at least min_cost, heaviest first (ties: lower slot first), and mark each of them in
  * `cost` with UINT32_MAX -- the value rt_lane_plan treats as "not in this map".  Returns the number

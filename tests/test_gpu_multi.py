@@ -115,12 +115,13 @@ def lane_costs(rt, s, w, h, spp, bounces, mine, n, r):
     return cost.cpu().numpy()
 
 
-@pytest.mark.parametrize("n,mode", [(1, "plan"), (4, "plan"), (2, "random")])
+@pytest.mark.parametrize("n,mode", [(1, "plan"), (4, "plan"), (2, "random"), (4, "refine")])
 def test_lane_map_shards_equal_full(rt, n, mode):
     """Probe per-pixel work -> rt_lane_plan (aggressive: every sub-tile wave above the costliest
-    pixel's modelled time is split) or a random permutation with idle lanes -> the sharded frames
-    rendered through the lane map == the unsharded frames, bit for bit (pixels, RNG progression
-    over two progressive frames)."""
+    pixel's modelled time is split; "refine": then rt_lane_refine from a timing frame's per-wave
+    clocks of that map, as bench.py --lane-refine does) or a random permutation with idle lanes ->
+    the sharded frames rendered through the lane map == the unsharded frames, bit for bit (pixels,
+    RNG progression over two progressive frames)."""
     w, h, spp, bounces, frames = 120, 72, 2, 6, 2
     full, _ = full_frames(rt, w, h, spp, bounces, frames)
     s = scene(rt, w, h)
@@ -135,9 +136,20 @@ def test_lane_map_shards_equal_full(rt, n, mode):
         xs, ys = rt.sharding.slot_pixels(w, h, r, n, int(counts[r]), lists[r, : counts[r]])
         inside = (xs >= 0) & (xs < w) & (ys >= 0) & (ys < h)
         assert (c[inside] > 0).all() and (c[~inside] == 0).all(), "work is reported for exactly the frame's pixels"
-        if mode == "plan":
+        if mode in ("plan", "refine"):
             m, nlong = rt.lane_plan(c, 1e12, 1.0)
             assert m.size > c.size, "the heavy sub-tile waves were split"
+        if mode == "refine":
+            rng = rt.alloc_rng(cap * 256)
+            rt.init_rng_tiles(rng, w, h, mine, T.SEED)
+            s.upload(rng.data_ptr())
+            clk = torch.zeros(m.size // 64, dtype=torch.int64, device="cuda")
+            rt.render(s, None, None, w, h, spp, bounces, 0, r, n, out_shard=shards[0, r], tile_list=mine,
+                      lane_slots=torch.from_numpy(m).cuda(), wave_clock=clk)
+            torch.cuda.synchronize()
+            m2, nsplit = rt.lane_refine(m, c, np.maximum(clk.cpu().numpy(), 0), 0.5)
+            assert nsplit > 0 and m2.size > m.size
+            m, nlong = m2, 0
         else:
             m = np.full(c.size * 2, -1, dtype=np.int32)
             m[gen.choice(m.size, c.size, replace=False)] = gen.permutation(c.size).astype(np.int32)

@@ -114,3 +114,55 @@ def test_lone_plan_takes_the_heaviest_and_lane_plan_skips_them(rt):
     assert few.size == 10 and (cost[few] == 5000).all()
     none, same = rt.lone_plan(cost, 10, 6000)
     assert none.size == 0 and np.array_equal(same, cost)
+
+
+def test_lane_refine_splits_the_measured_tail(rt):
+    """rt_lane_refine: the waves whose measured clock is within theta of the longest (and hold more
+    than one pixel) become two waves, their pixels in decreasing work dealt alternately; every slot
+    stays mapped exactly once and the waves come out longest first (a half at 3/4 of its parent)."""
+    gen = np.random.default_rng(5)
+    slots = 64 * 40
+    cost = gen.integers(1, 1000, slots).astype(np.uint32)
+    m, _ = rt.lane_plan(cost, 1e12, 1.0)
+    nw = m.size // 64
+    ticks = gen.integers(100, 1000, nw).astype(np.int64)
+    ticks[3], ticks[7] = 5000, 4000  # the measured tail: waves 3 and 7 (within 0.75 of the longest)
+    lone = np.flatnonzero((m.reshape(-1, 64) >= 0).sum(1) == 1)
+    if lone.size:  # a one-pixel wave in the tail stays whole
+        ticks[lone[0]] = 4500
+    out, nsplit = rt.lane_refine(m, cost, ticks, 0.75)
+    check_perm(out, slots)
+    assert nsplit == 4 and out.size == m.size + 2 * 64
+    rows = [r[r >= 0] for r in out.reshape(-1, 64)]
+    for w in (3, 7):
+        px = m.reshape(-1, 64)[w]
+        px = px[px >= 0]
+        by = px[np.argsort(-cost[px].astype(np.int64), kind="stable")]
+        halves = [list(by[0::2]), list(by[1::2])]
+        assert sum(list(r) in halves for r in rows) == 2, w
+    # waves kept whole come out longest first (the lone-pixel wave at 4,500 ticks ahead of all)
+    est = {}
+    mw = m.reshape(-1, 64)
+    for w in range(nw):
+        px = tuple(sorted(mw[w][mw[w] >= 0]))
+        est[px] = float(ticks[w])
+    got = [est.get(tuple(sorted(r)), None) for r in rows]
+    whole = [g for g in got if g is not None]
+    assert whole == sorted(whole, reverse=True)
+    if lone.size:
+        assert got[0] == 4500.0
+
+
+def test_lane_refine_bad_arguments(rt):
+    m = np.arange(128, dtype=np.int32)
+    cost = np.ones(128, dtype=np.uint32)
+    with pytest.raises(rt.RTError, match="lane_refine"):
+        rt.lane_refine(m, cost, np.array([1, -1]), 0.75)  # negative clock
+    with pytest.raises(rt.RTError, match="lane_refine"):
+        rt.lane_refine(m, cost, np.array([1, 2]), 0.0)  # theta must be > 0
+    bad = m.copy()
+    bad[5] = 128
+    with pytest.raises(rt.RTError, match="lane_refine"):
+        rt.lane_refine(bad, cost, np.array([1, 2]), 0.75)  # slot outside the shard
+    same, nsplit = rt.lane_refine(m, cost, np.zeros(2, dtype=np.int64), 0.75)  # nothing measured: no split
+    assert nsplit == 0 and np.array_equal(same, m)

@@ -38,6 +38,7 @@ def probe(rt, scene, W, H, SPP, BOUNCES):
 
 
 TUNE, WPS, SPLIT, LONE, LONE_MIN = 0, 0, 1, 0, 1  # --tune / --wps / --split / --lone / --lone-min
+REFINE, THETA = 0, 0.75  # --refine / --theta: bench.refine_lane_map rounds after the lane plan
 
 
 def lane_map(rt, scene, W, H, SPP, BOUNCES, mine, rng, lane):
@@ -58,6 +59,12 @@ def lane_map(rt, scene, W, H, SPP, BOUNCES, mine, rng, lane):
     m, nlong = rt.lane_plan(c, lane[0], lane[1])
     nlong = int(lane[2]) if len(lane) >= 3 else nlong  # lane[2]: the number of leading waves at raised priority
     rt.init_rng_tiles(rng, W, H, mine, bench.SEED)
+    if REFINE:  # the bench's measured refinement (rt_lane_refine), same frames, same RNG copies
+        def frame(**kw):
+            rt.render(scene, None, None, W, H, SPP, BOUNCES, 0, 0, 1, out_shard=out, tile_list=mine, **kw)
+        m, info = bench.refine_lane_map(rt, frame, rng, m, c, REFINE, THETA, "cuda", waves_per_simd=WPS or 6)
+        print(json.dumps({"refine": info, "waves": int(m.size // 64)}), flush=True)
+        nlong = 0
     lm = torch.from_numpy(m).cuda()
     if os.environ.get("LANE_DIAG"):  # which waves are the long ones under this plan
         clk = torch.zeros(m.size // 64, dtype=torch.int64, device="cuda")
@@ -115,9 +122,11 @@ def main():
     ap.add_argument("--split", type=int, default=1, help="split every 8x8 wave into this many waves (1, 2, 4)")
     ap.add_argument("--lone", default="0", help="comma list of lone-pixel counts per shard to try (rt_lone_plan)")
     ap.add_argument("--lone-min", type=int, default=1, help="rt_lone_plan min_cost")
+    ap.add_argument("--refine", type=int, default=0, help="rounds of measured lane-plan refinement (bench --lane-refine)")
+    ap.add_argument("--theta", type=float, default=0.75, help="rt_lane_refine theta (bench --lane-theta)")
     args = ap.parse_args()
-    global TUNE, WPS, SPLIT, LONE, LONE_MIN
-    TUNE, WPS, SPLIT, LONE_MIN = args.tune, args.wps, args.split, args.lone_min
+    global TUNE, WPS, SPLIT, LONE, LONE_MIN, REFINE, THETA
+    TUNE, WPS, SPLIT, LONE_MIN, REFINE, THETA = args.tune, args.wps, args.split, args.lone_min, args.refine, args.theta
     lone_list = [int(x) for x in args.lone.split(",")]
     rt = G.load_package()
     scene_name, W0, H0, SPP, BOUNCES, _ = bench.CONFIGS[args.config]
