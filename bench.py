@@ -433,7 +433,7 @@ def make_plan(rt, scene, W, H, SPP, BOUNCES, rank, world, plan_kind, dev):
                            "invalid_wave_clocks": nbad}
 
 
-def make_lane_map(rt, render, rng, slots, units, dev, refine=0, theta=0.75):
+def make_lane_map(rt, render, rng, slots, units, dev, refine=0, theta=0.85):
     """rt_lane_plan for this rank's list: one probe frame of per-pixel work (timing variant of the
     production kernel, set-up, untimed) on a copy of the RNG states, then the split plan, then up to
     `refine` rounds of measured refinement (refine_lane_map).  Returns (device int32 lane map, info)."""
@@ -456,34 +456,39 @@ def make_lane_map(rt, render, rng, slots, units, dev, refine=0, theta=0.75):
     return torch.from_numpy(lm).to(dev), info
 
 
-def refine_lane_map(rt, render, rng, lm, cost, rounds, theta, dev, waves_per_simd=6):
-    """Measured lane-plan refinement (rt_lane_refine): time a frame of the map (production kernel, HIP
-    events, best of two, on a copy of the RNG states), take one timing frame's per-wave clocks, split
-    the waves within `theta` of the longest, and keep the new map only while the frame gets faster.
-    Config 2 at N = 8, shard by shard: 5.93 -> 4.56 ms in one round (profiles/r03e_lane_refine.jsonl).
-    Every candidate is a permutation of the shard's slots, so the frame is the same bit for bit."""
+def refine_lane_map(rt, render, rng, lm, cost, rounds, theta, dev, waves_per_simd=6, frames=3):
+    """Measured lane-plan refinement (rt_lane_refine): time `frames` consecutive frames of the map
+    (production kernel, HIP events, the RNG chain advancing from a saved copy of the states as the
+    run's frames will), sum each wave's clocks over the same frames (timing variant), split the waves
+    within `theta` of the longest, and keep the new map only while those frames get faster.  Several
+    frames, not one: which waves are slow changes from frame to frame with the random paths, and a
+    plan fitted to one frame's tail does not carry over.  Every candidate is a permutation of the
+    shard's slots, so the frames are the same bit for bit."""
     import torch
 
     saved = rng.clone()
 
     def timed(m_dev):
-        best = 1e30
-        for _ in range(2):
+        total = 0.0
+        for _ in range(frames):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             render(lane_slots=m_dev, waves_per_simd=waves_per_simd)
             e1.record()
             torch.cuda.synchronize()
-            rng.copy_(saved)
-            best = min(best, e0.elapsed_time(e1))
-        return best
+            total += e0.elapsed_time(e1)
+        rng.copy_(saved)
+        return total / frames
 
     def clocks(m_dev):
+        acc = np.zeros(m_dev.numel() // 64, dtype=np.int64)
         clk = torch.zeros(m_dev.numel() // 64, dtype=torch.int64, device=dev)
-        render(lane_slots=m_dev, wave_clock=clk)
-        torch.cuda.synchronize()
+        for _ in range(frames):
+            render(lane_slots=m_dev, wave_clock=clk)
+            torch.cuda.synchronize()
+            acc += sanitize_wave_clocks(clk.cpu().numpy())[0].astype(np.int64)
         rng.copy_(saved)
-        return sanitize_wave_clocks(clk.cpu().numpy())[0]
+        return acc
 
     t0 = time.perf_counter()
     cur, cur_dev = lm, torch.from_numpy(lm).to(dev)
@@ -497,8 +502,15 @@ def refine_lane_map(rt, render, rng, lm, cost, rounds, theta, dev, waves_per_sim
         if not nsplit or ms >= best_ms:
             break
         cur, cur_dev, best_ms, kept = new, new_dev, ms, kept + 1
+    # where the kept map's time goes: its longest waves (summed clocks over the frames, ms per frame)
+    # and how many pixels each holds
+    ticks = clocks(cur_dev)
+    top = np.argsort(-ticks)[:6]
+    mw = cur.reshape(-1, 64)
+    longest = [[round(float(ticks[w]) / frames / CLOCK_HZ * 1e3, 3), int((mw[w] >= 0).sum())] for w in top]
     del saved
-    return cur, {"theta": theta, "frame_ms": hist, "rounds_kept": kept, "s": round(time.perf_counter() - t0, 3)}
+    return cur, {"theta": theta, "frames": frames, "frame_ms": hist, "rounds_kept": kept,
+                 "longest_waves_ms_pixels": longest, "s": round(time.perf_counter() - t0, 3)}
 
 
 def run(args):
@@ -858,9 +870,9 @@ def main():
                          "auto = time one untimed frame at 5 / 6 / 7 (N > 1: also 3 / 4) and keep the fastest")
     ap.add_argument("--lanes", default="auto", choices=["auto", "on", "off"],
                     help="lane plan (rt_lane_plan: split the waves of the frame's costliest pixels); auto = on for N > 1")
-    ap.add_argument("--lane-refine", type=int, default=3,
+    ap.add_argument("--lane-refine", type=int, default=5,
                     help="N > 1: rounds of measured lane-plan refinement (rt_lane_refine; 0 = the model's plan only)")
-    ap.add_argument("--lane-theta", type=float, default=0.75,
+    ap.add_argument("--lane-theta", type=float, default=0.85,
                     help="rt_lane_refine theta: waves measured within this fraction of the longest are split")
     ap.add_argument("--lane-units", type=float, default=48000.0,
                     help="rt_lane_plan parallel_units (MI355X: 48000 measured best for configs 2 and 3 at N = 2-8)")

@@ -38,7 +38,8 @@ def probe(rt, scene, W, H, SPP, BOUNCES):
 
 
 TUNE, WPS, SPLIT, LONE, LONE_MIN = 0, 0, 1, 0, 1  # --tune / --wps / --split / --lone / --lone-min
-REFINE, THETA = 0, 0.75  # --refine / --theta: bench.refine_lane_map rounds after the lane plan
+SKIP_NO_LANE = bool(os.environ.get("SKIP_NO_LANE"))  # only the lane-plan rows
+REFINE, THETA = 0, 0.85  # --refine / --theta: bench.refine_lane_map rounds after the lane plan
 
 
 def lane_map(rt, scene, W, H, SPP, BOUNCES, mine, rng, lane):
@@ -123,7 +124,7 @@ def main():
     ap.add_argument("--lone", default="0", help="comma list of lone-pixel counts per shard to try (rt_lone_plan)")
     ap.add_argument("--lone-min", type=int, default=1, help="rt_lone_plan min_cost")
     ap.add_argument("--refine", type=int, default=0, help="rounds of measured lane-plan refinement (bench --lane-refine)")
-    ap.add_argument("--theta", type=float, default=0.75, help="rt_lane_refine theta (bench --lane-theta)")
+    ap.add_argument("--theta", type=float, default=0.85, help="rt_lane_refine theta (bench --lane-theta)")
     args = ap.parse_args()
     global TUNE, WPS, SPLIT, LONE, LONE_MIN, REFINE, THETA
     TUNE, WPS, SPLIT, LONE_MIN, REFINE, THETA = args.tune, args.wps, args.split, args.lone_min, args.refine, args.theta
@@ -136,6 +137,8 @@ def main():
     lanes = [None] + [tuple(map(float, x.split(":"))) for x in args.lanes.split(";") if x]
     plans = [(p, l, k) for p in args.plans.split(",") for l in lanes for k in (lone_list if l else [0])]
     for plan, lane, lone_k in plans:
+        if lane is None and SKIP_NO_LANE:
+            continue
         LONE = lone_k
         per_n = {}
         for n in map(int, args.ns.split(",")):
