@@ -415,10 +415,15 @@ size_t cap_lds_bytes(K kernel, int cap) {
 }
 
 template <class K>
-hipError_t launch_grid(K kernel, const RenderArgs& args, int waves, bool refill, hipStream_t stream, size_t lds = 0) {
+hipError_t launch_grid(K kernel, const RenderArgs& args, int waves, bool refill, hipStream_t stream, size_t lds = 0,
+                       int cap = 0) {
     int grid = waves;
     if (refill && args.queue_head) {  // refill variants: one grid of resident waves, the rest through the queue
-        const int res = resident_waves(kernel);
+        int res = resident_waves(kernel);
+        int dev = 0, cus = 0;
+        if (cap > 0 && hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+            res = std::min(res, cap * 4 * cus);  // the residency cap holds fewer
         if (res > 0) grid = std::min(waves, res);
     }
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(WAVE), lds, stream, args);
@@ -438,7 +443,7 @@ hipError_t launch_occ(const RenderArgs& args, int waves, hipStream_t stream) {
         const int w = t == 2u ? 6 : t == 3u ? 7 : args.waves_per_simd;
         if (w >= 1 && w <= 4) {  // the 5-wave build, residency capped by dynamic LDS
             const auto k = render_fast_kernel_w5<STACK, false, MODE>;
-            return launch_grid(k, args, waves, refill, stream, cap_lds_bytes(k, w));
+            return launch_grid(k, args, waves, refill, stream, cap_lds_bytes(k, w), w);
         }
         if (w == 7) return launch_grid(render_fast_kernel_w7<STACK, false, MODE>, args, waves, refill, stream);
         return w == 6 ? launch_grid(render_fast_kernel_w6<STACK, false, MODE>, args, waves, refill, stream)

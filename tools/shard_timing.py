@@ -39,6 +39,7 @@ def probe(rt, scene, W, H, SPP, BOUNCES):
 
 TUNE, WPS, SPLIT, LONE, LONE_MIN = 0, 0, 1, 0, 1  # --tune / --wps / --split / --lone / --lone-min
 SKIP_NO_LANE = bool(os.environ.get("SKIP_NO_LANE"))  # only the lane-plan rows
+REFILL = 0  # --refill: rt_render refill_lanes of the timed frames
 REFINE, THETA = 0, 0.85  # --refine / --theta: bench.refine_lane_map rounds after the lane plan
 
 
@@ -102,7 +103,8 @@ def time_shard(rt, scene, W, H, SPP, BOUNCES, tiles, r, n, reps, lane=None):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         rt.render(scene, None, bufs[(i + 1) & 1], W, H, SPP, BOUNCES, i, r, n, out_shard=bufs[i & 1], tile_list=mine,
-                  lane_slots=lm, priority_waves=nlong, tune=TUNE, waves_per_simd=WPS, lone_slots=lone)
+                  lane_slots=lm, priority_waves=nlong, tune=TUNE, waves_per_simd=WPS, lone_slots=lone,
+                  refill_lanes=REFILL)
         e1.record()
         torch.cuda.synchronize()
         if i:
@@ -123,10 +125,12 @@ def main():
     ap.add_argument("--split", type=int, default=1, help="split every 8x8 wave into this many waves (1, 2, 4)")
     ap.add_argument("--lone", default="0", help="comma list of lone-pixel counts per shard to try (rt_lone_plan)")
     ap.add_argument("--lone-min", type=int, default=1, help="rt_lone_plan min_cost")
+    ap.add_argument("--refill", type=int, default=0, help="rt_render refill_lanes of the timed frames (0 = off)")
     ap.add_argument("--refine", type=int, default=0, help="rounds of measured lane-plan refinement (bench --lane-refine)")
     ap.add_argument("--theta", type=float, default=0.85, help="rt_lane_refine theta (bench --lane-theta)")
     args = ap.parse_args()
-    global TUNE, WPS, SPLIT, LONE, LONE_MIN, REFINE, THETA
+    global TUNE, WPS, SPLIT, LONE, LONE_MIN, REFINE, THETA, REFILL
+    REFILL = args.refill
     TUNE, WPS, SPLIT, LONE_MIN, REFINE, THETA = args.tune, args.wps, args.split, args.lone_min, args.refine, args.theta
     lone_list = [int(x) for x in args.lone.split(",")]
     rt = G.load_package()
