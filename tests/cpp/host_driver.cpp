@@ -10,10 +10,12 @@
 // rt_gather_shards (RCCL, communicators from rt_comm_init_all) brings the shards to device 0,
 // where rt_unshard_tiles writes the pitched surface.  Before the first frame every device runs
 // one probe frame of per-pixel work (rt_render_params.lane_cost, on a copy of its RNG states)
-// and renders through the lane map rt_lane_plan builds from it (bench.py's N > 1 default).
+// and renders through the lane map rt_lane_plan builds from it, refined once by rt_lane_refine from
+// the per-wave clocks of a timing frame of that map (bench.py's N > 1 default).
 //
 //   g++ -std=c++17 -Iinclude tests/cpp/host_driver.cpp -Lcuda-raytracing_amd -lrt_hip -o host_driver
 //   ./host_driver out.bin W H frames assets_dir [split]
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -134,6 +136,48 @@ static int run_split(const char* path, int w, int h, int frames, const char* ass
         if (r.lanes <= 0) CHECK(1);
         CHECK(rt_malloc(&r.lane_map, (size_t)r.lanes * 4));
         CHECK(rt_memcpy_h2d(r.lane_map, map.data(), (size_t)r.lanes * 4));
+        // one round of measured refinement (bench.py refine_lane_map): per-wave clocks of a timing
+        // frame of the map, rt_lane_refine, and the refined map kept only if a frame of it is faster
+        {
+            const int64_t waves = r.lanes / 64;
+            void* clk_dev = nullptr;
+            CHECK(rt_malloc(&clk_dev, (size_t)waves * 8));
+            p.lane_cost = nullptr;
+            p.lane_slots = (const int32_t*)r.lane_map, p.lane_slot_count = r.lanes;
+            p.wave_clock = (uint64_t*)clk_dev;
+            CHECK(rt_render(&p, rt_scene_gpu(r.scene), nullptr));
+            std::vector<int64_t> ticks((size_t)waves);
+            CHECK(rt_memcpy_d2h(ticks.data(), clk_dev, ticks.size() * 8));
+            CHECK(rt_memcpy_d2d(r.rng, rng_copy, (size_t)slots * 48));
+            for (int64_t& t : ticks) t = t < 0 ? 0 : t;  // device-clock deltas: never negative, guarded anyway
+            std::vector<int32_t> map2((size_t)(2 * r.lanes));
+            int64_t nsplit = 0;
+            const int64_t n2 = rt_lane_refine(map.data(), r.lanes, cost.data(), slots, ticks.data(), 0.85, map2.data(),
+                                              (int64_t)map2.size(), &nsplit);
+            if (n2 <= 0) CHECK(1);
+            void* map2_dev = nullptr;
+            CHECK(rt_malloc(&map2_dev, (size_t)n2 * 4));
+            CHECK(rt_memcpy_h2d(map2_dev, map2.data(), (size_t)n2 * 4));
+            p.wave_clock = nullptr;
+            auto frame_s = [&](void* m, int64_t entries) {
+                p.lane_slots = (const int32_t*)m, p.lane_slot_count = entries;
+                CHECK(rt_synchronize());
+                const auto t0 = std::chrono::steady_clock::now();
+                CHECK(rt_render(&p, rt_scene_gpu(r.scene), nullptr));
+                CHECK(rt_synchronize());
+                const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                CHECK(rt_memcpy_d2d(r.rng, rng_copy, (size_t)slots * 48));
+                return s;
+            };
+            if (nsplit > 0 && frame_s(map2_dev, n2) < frame_s(r.lane_map, r.lanes)) {
+                rt_free(r.lane_map);
+                r.lane_map = map2_dev, r.lanes = n2;
+            } else {
+                rt_free(map2_dev);
+            }
+            rt_free(clk_dev);
+            CHECK(rt_memset(r.shard[0], 0, shard_bytes));
+        }
         rt_free(rng_copy);
         rt_free(cost_dev);
     }
