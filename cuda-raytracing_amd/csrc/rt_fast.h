@@ -1132,7 +1132,13 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                     if (nI + nL == 1 && (tune & (1u << 26)) == 0) {
                         const int r = __ffsll((long long)(mI | mL)) - 1;
                         if (__builtin_amdgcn_readlane(T.sp, r) <= S::LDS_ENTRIES) {
+#ifdef RT_LANE_HIST  // diagnostic build (tools/lane_hist.sh): wave cycles of the lone-lane tails
+                            const unsigned long long tl0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+#endif
                             lone_traverse(nodes4, tris, stk, r, R, h, T, active);
+#ifdef RT_LANE_HIST
+                            if (TIMING) c.cy_ttri += __builtin_amdgcn_s_memtime() - tl0;
+#endif
                             continue;
                         }
                     }
@@ -1140,6 +1146,9 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                 // leaf step when nL * 4 >= nI * (q + 1); q = 1 measured best (RT_TUNE bits 13-15: q + 1)
                 const uint32_t qv = (tune >> 13) & 7u, q = qv ? qv - 1u : 1u;
                 if (TIMING) c.w_small++, c.l_small += inner || leafs;
+#ifdef RT_LANE_HIST  // diagnostic build: wave cycles of small-step iterations by active-lane count
+                const unsigned long long th0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+#endif
                 if (!mI || nL * 4u >= nI * (q + 1u)) {
                     if (leafs) {
                         active = small_step<STATS>(nodes4, tris, spairs, stk, R, h, T, c);
@@ -1149,6 +1158,16 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                     active = small_step<STATS>(nodes4, tris, spairs, stk, R, h, T, c);
                     if (TIMING) c.lane_work++;
                 }
+#ifdef RT_LANE_HIST
+                if (TIMING) {
+                    const unsigned long long dt = __builtin_amdgcn_s_memtime() - th0;
+                    const uint32_t n = nI + nL;
+                    c.ktest += n <= 4u ? dt : 0ull;            // 1-4 active lanes
+                    c.ktri += (n > 4u && n <= 16u) ? dt : 0ull;  // 5-16
+                    c.cy_tcl += dt;                            // every small-step iteration
+                    c.r_shared += n <= 4u;                     // iterations with 1-4 lanes
+                }
+#endif
                 continue;
             }
         }
