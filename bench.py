@@ -278,6 +278,11 @@ def pmc_pass(args, out_dir, timeout_s=150):
                "--lanes", args.lanes, "--lane-units", str(args.lane_units), "--occupancy", str(args.occupancy_chosen)]
         if args.foreign:
             cmd.append("--foreign")
+        if getattr(args, "lane_map_np", None) is not None:
+            os.makedirs(out_dir, exist_ok=True)
+            mp = os.path.join(out_dir, "lane_map.npy")
+            np.save(mp, args.lane_map_np)
+            cmd += ["--lane-map-file", mp]
         if args.build_options:
             cmd += ["--build-options", args.build_options]
         try:
@@ -452,6 +457,9 @@ def make_lane_map(rt, render, rng, slots, units, dev, refine=0, theta=0.85):
     info = {"lane_probe_s": round(probe_s, 4), "waves": int(lm.size // 64), "long_waves": nlong, "parallel_units": units}
     if refine > 0:
         lm, info["refine"] = refine_lane_map(rt, render, rng, lm, cost_np, refine, theta, dev)
+        if lm is None:  # the plain tile order won
+            info["waves"] = 0
+            return None, info
         info["waves"] = int(lm.size // 64)
     return torch.from_numpy(lm).to(dev), info
 
@@ -502,6 +510,13 @@ def refine_lane_map(rt, render, rng, lm, cost, rounds, theta, dev, waves_per_sim
         if not nsplit or ms >= best_ms:
             break
         cur, cur_dev, best_ms, kept = new, new_dev, ms, kept + 1
+    # the plain tile order over the same frames: a lane map is kept only if it beats it
+    plain_ms = timed(None)
+    if plain_ms <= best_ms:
+        del saved
+        return None, {"theta": theta, "frames": frames, "frame_ms": hist, "rounds_kept": kept,
+                      "plain_ms": round(plain_ms, 3), "map": "dropped (the plain tile order is faster)",
+                      "s": round(time.perf_counter() - t0, 3)}
     # where the kept map's time goes: its longest waves (summed clocks over the frames, ms per frame)
     # and how many pixels each holds
     ticks = clocks(cur_dev)
@@ -510,7 +525,8 @@ def refine_lane_map(rt, render, rng, lm, cost, rounds, theta, dev, waves_per_sim
     longest = [[round(float(ticks[w]) / frames / CLOCK_HZ * 1e3, 3), int((mw[w] >= 0).sum())] for w in top]
     del saved
     return cur, {"theta": theta, "frames": frames, "frame_ms": hist, "rounds_kept": kept,
-                 "longest_waves_ms_pixels": longest, "s": round(time.perf_counter() - t0, 3)}
+                 "plain_ms": round(plain_ms, 3), "longest_waves_ms_pixels": longest,
+                 "s": round(time.perf_counter() - t0, 3)}
 
 
 def run(args):
@@ -603,14 +619,18 @@ def run(args):
         return kw if args.foreign else dict(kw, refill_lanes=args.refill)
 
     # lane plan (rt_lane_plan): split the waves whose pixels form the frame's serial tail
-    lanes_on = args.lanes == "on" or (args.lanes == "auto" and sharded)
-    if lanes_on and not args.foreign and tile_list is not None:
+    lanes_on = args.lanes in ("on", "auto")
+    if lanes_on and not args.foreign and tile_list is not None and args.lane_map_file:
+        # PMC child: the parent's final lane map, so the counters are of exactly the frames it timed
+        lane_slots = torch.from_numpy(np.load(args.lane_map_file)).to(dev)
+    elif lanes_on and not args.foreign and tile_list is not None:
         t1 = time.perf_counter()
         lane_slots, lane_info = make_lane_map(rt, lambda **kw: render(0, bufs[0], None, **kw), rng,
                                               tile_list.numel() * 256, args.lane_units, dev,
-                                              refine=args.lane_refine if sharded else 0, theta=args.lane_theta)
+                                              refine=args.lane_refine, theta=args.lane_theta)
         setup_s += time.perf_counter() - t1
         plan_info = dict(plan_info or {}, lanes=lane_info)
+    args.lane_map_np = lane_slots.cpu().numpy() if lane_slots is not None else None
 
     # occupancy (rt_render_params.waves_per_simd): time one untimed frame at 5, 6 and 7 waves per
     # SIMD (twice each, on a copy of the RNG states) and keep the fastest; a strong-scaled shard
@@ -869,9 +889,11 @@ def main():
                     help="rt_render waves_per_simd (1-4: the 5-wave build capped at that residency by dynamic LDS); "
                          "auto = time one untimed frame at 5 / 6 / 7 (N > 1: also 3 / 4) and keep the fastest")
     ap.add_argument("--lanes", default="auto", choices=["auto", "on", "off"],
-                    help="lane plan (rt_lane_plan: split the waves of the frame's costliest pixels); auto = on for N > 1")
+                    help="lane plan (rt_lane_plan: split the waves of the frame's costliest pixels, then --lane-refine "
+                         "rounds of measured refinement); auto = on (config 2 at N = 1: 14.1-14.3 vs 15.5-15.8 ms)")
+    ap.add_argument("--lane-map-file", default=None, help=argparse.SUPPRESS)  # PMC child: the parent's lane map
     ap.add_argument("--lane-refine", type=int, default=5,
-                    help="N > 1: rounds of measured lane-plan refinement (rt_lane_refine; 0 = the model's plan only)")
+                    help="rounds of measured lane-plan refinement whenever a lane plan is on (rt_lane_refine; 0 = the model's plan only)")
     ap.add_argument("--lane-theta", type=float, default=0.85,
                     help="rt_lane_refine theta: waves measured within this fraction of the longest are split")
     ap.add_argument("--lane-units", type=float, default=48000.0,

@@ -65,8 +65,10 @@ def lane_map(rt, scene, W, H, SPP, BOUNCES, mine, rng, lane):
         def frame(**kw):
             rt.render(scene, None, None, W, H, SPP, BOUNCES, 0, 0, 1, out_shard=out, tile_list=mine, **kw)
         m, info = bench.refine_lane_map(rt, frame, rng, m, c, REFINE, THETA, "cuda", waves_per_simd=WPS or 6)
-        print(json.dumps({"refine": info, "waves": int(m.size // 64)}), flush=True)
+        print(json.dumps({"refine": info, "waves": int(m.size // 64) if m is not None else 0}), flush=True)
         nlong = 0
+        if m is None:  # the plain tile order won
+            return None, 0, lone
     lm = torch.from_numpy(m).cuda()
     if os.environ.get("LANE_DIAG"):  # which waves are the long ones under this plan
         clk = torch.zeros(m.size // 64, dtype=torch.int64, device="cuda")
