@@ -438,7 +438,7 @@ def make_plan(rt, scene, W, H, SPP, BOUNCES, rank, world, plan_kind, dev):
                            "invalid_wave_clocks": nbad}
 
 
-def make_lane_map(rt, render, rng, slots, units, dev, refine=0, theta=0.85):
+def make_lane_map(rt, render, rng, slots, units, dev, refine=0, theta=0.85, waves_per_simd=6):
     """rt_lane_plan for this rank's list: one probe frame of per-pixel work (timing variant of the
     production kernel, set-up, untimed) on a copy of the RNG states, then the split plan, then up to
     `refine` rounds of measured refinement (refine_lane_map).  Returns (device int32 lane map, info)."""
@@ -456,7 +456,7 @@ def make_lane_map(rt, render, rng, slots, units, dev, refine=0, theta=0.85):
     lm, nlong = rt.lane_plan(cost_np, units, 1.0)
     info = {"lane_probe_s": round(probe_s, 4), "waves": int(lm.size // 64), "long_waves": nlong, "parallel_units": units}
     if refine > 0:
-        lm, info["refine"] = refine_lane_map(rt, render, rng, lm, cost_np, refine, theta, dev)
+        lm, info["refine"] = refine_lane_map(rt, render, rng, lm, cost_np, refine, theta, dev, waves_per_simd)
         if lm is None:  # the plain tile order won
             info["waves"] = 0
             return None, info
@@ -464,7 +464,7 @@ def make_lane_map(rt, render, rng, slots, units, dev, refine=0, theta=0.85):
     return torch.from_numpy(lm).to(dev), info
 
 
-def refine_lane_map(rt, render, rng, lm, cost, rounds, theta, dev, waves_per_simd=6, frames=3):
+def refine_lane_map(rt, render, rng, lm, cost, rounds, theta, dev, waves_per_simd, frames=3):
     """Measured lane-plan refinement (rt_lane_refine): time `frames` consecutive frames of the map
     (production kernel, HIP events, the RNG chain advancing from a saved copy of the states as the
     run's frames will), sum each wave's clocks over the same frames (timing variant), split the waves
@@ -514,7 +514,7 @@ def refine_lane_map(rt, render, rng, lm, cost, rounds, theta, dev, waves_per_sim
     plain_ms = timed(None)
     if plain_ms <= best_ms:
         del saved
-        return None, {"theta": theta, "frames": frames, "frame_ms": hist, "rounds_kept": kept,
+        return None, {"theta": theta, "frames": frames, "waves_per_simd": waves_per_simd, "frame_ms": hist, "rounds_kept": kept,
                       "plain_ms": round(plain_ms, 3), "map": "dropped (the plain tile order is faster)",
                       "s": round(time.perf_counter() - t0, 3)}
     # where the kept map's time goes: its longest waves (summed clocks over the frames, ms per frame)
@@ -524,7 +524,7 @@ def refine_lane_map(rt, render, rng, lm, cost, rounds, theta, dev, waves_per_sim
     mw = cur.reshape(-1, 64)
     longest = [[round(float(ticks[w]) / frames / CLOCK_HZ * 1e3, 3), int((mw[w] >= 0).sum())] for w in top]
     del saved
-    return cur, {"theta": theta, "frames": frames, "frame_ms": hist, "rounds_kept": kept,
+    return cur, {"theta": theta, "frames": frames, "waves_per_simd": waves_per_simd, "frame_ms": hist, "rounds_kept": kept,
                  "plain_ms": round(plain_ms, 3), "longest_waves_ms_pixels": longest,
                  "s": round(time.perf_counter() - t0, 3)}
 
@@ -541,6 +541,8 @@ def run(args):
     wd.phase = "scene set-up and plans"
     assert world == args.gpus or args.pmc_child, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     rt = G.load_package()
+    if args.tracer != "fast" or args.refill or (args.tune & 0x1030):
+        rt.load_experimental()  # A/B render paths (librt_hip_exp.so); the production path never needs it
     if args.build_options:  # exact-preserving mirror / BVH builder knobs (rt_set_build_options)
         rt.set_build_options(**{k: float(v) if k == "split_angle" else int(v)
                                 for k, v in (kv.split("=") for kv in args.build_options.split(","))})
@@ -618,33 +620,19 @@ def run(args):
         kw = dict(occupancy, **kw)
         return kw if args.foreign else dict(kw, refill_lanes=args.refill)
 
-    # lane plan (rt_lane_plan): split the waves whose pixels form the frame's serial tail
-    lanes_on = args.lanes in ("on", "auto")
-    if lanes_on and not args.foreign and tile_list is not None and args.lane_map_file:
-        # PMC child: the parent's final lane map, so the counters are of exactly the frames it timed
-        lane_slots = torch.from_numpy(np.load(args.lane_map_file)).to(dev)
-    elif lanes_on and not args.foreign and tile_list is not None:
-        t1 = time.perf_counter()
-        lane_slots, lane_info = make_lane_map(rt, lambda **kw: render(0, bufs[0], None, **kw), rng,
-                                              tile_list.numel() * 256, args.lane_units, dev,
-                                              refine=args.lane_refine, theta=args.lane_theta)
-        setup_s += time.perf_counter() - t1
-        plan_info = dict(plan_info or {}, lanes=lane_info)
-    args.lane_map_np = lane_slots.cpu().numpy() if lane_slots is not None else None
-
     # occupancy (rt_render_params.waves_per_simd): time one untimed frame at 5, 6 and 7 waves per
     # SIMD (twice each, on a copy of the RNG states) and keep the fastest; a strong-scaled shard
     # (N > 1) also tries the 5-wave build capped at 3 and 4 resident waves per SIMD (dynamic LDS):
     # config 2 at N = 8, 6.36 ms at 4 vs 6.66 ms at 6 (profiles/r03e_capped_shards.jsonl)
-    if args.occupancy == "auto" and not args.pmc_child:
-        t1 = time.perf_counter()
+    cands = (5, 6, 7) if world == 1 else (3, 4, 5, 6, 7)
+
+    def probe_occupancy(ls):
         rng_saved = rng.clone()
         best = {}
-        cands = (5, 6, 7) if world == 1 else (3, 4, 5, 6, 7)
         for wps in cands + cands:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            render(0, bufs[0], None, waves_per_simd=wps)
+            render(0, bufs[0], None, waves_per_simd=wps, lane_slots=ls)
             e1.record(stream)
             torch.cuda.synchronize()
             rng.copy_(rng_saved)
@@ -656,11 +644,50 @@ def run(args):
             t = torch.tensor([best[w] for w in cands], dtype=torch.float64, device=cdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             best = {w: float(x) for w, x in zip(cands, t.tolist())}
-        occupancy["waves_per_simd"] = min(best, key=best.get)
+        return min(best, key=best.get), best
+
+    auto_occ = args.occupancy == "auto" and not args.pmc_child
+    lanes_on = args.lanes in ("on", "auto") and not args.foreign and tile_list is not None
+    refine_occ = None if args.occupancy == "auto" else int(args.occupancy)
+    if auto_occ and lanes_on and not args.lane_map_file and args.lane_refine > 0:
+        # the lane map is refined (and compared with the plain tile order) at the occupancy the
+        # frames will run at: a first probe on the plain order picks it
+        t1 = time.perf_counter()
+        refine_occ, first = probe_occupancy(None)
+        setup_s += time.perf_counter() - t1
+        plan_info = dict(plan_info or {}, occupancy_plain_order={"waves_per_simd": refine_occ,
+                                                                 "probe_ms": {str(k): round(v, 3) for k, v in first.items()}})
+
+    # lane plan (rt_lane_plan): split the waves whose pixels form the frame's serial tail
+    if lanes_on and args.lane_map_file:
+        # PMC child: the parent's final lane map, so the counters are of exactly the frames it timed
+        lane_slots = torch.from_numpy(np.load(args.lane_map_file)).to(dev)
+    elif lanes_on:
+        t1 = time.perf_counter()
+        lane_slots, lane_info = make_lane_map(rt, lambda **kw: render(0, bufs[0], None, **kw), rng,
+                                              tile_list.numel() * 256, args.lane_units, dev,
+                                              refine=args.lane_refine, theta=args.lane_theta,
+                                              waves_per_simd=refine_occ or 6)
+        setup_s += time.perf_counter() - t1
+        plan_info = dict(plan_info or {}, lanes=lane_info)
+
+    if auto_occ:
+        t1 = time.perf_counter()
+        occupancy["waves_per_simd"], best = probe_occupancy(lane_slots)
+        if lane_slots is not None and refine_occ is not None and occupancy["waves_per_simd"] != refine_occ:
+            # the map was kept against the plain order at another occupancy: compare again at this one
+            wps = occupancy["waves_per_simd"]
+            plain_wps, plain_best = probe_occupancy(None)
+            if plain_best[plain_wps] <= best[wps]:
+                lane_slots = None
+                occupancy["waves_per_simd"] = plain_wps
+                plan_info["lanes"]["map"] = f"dropped at {wps} waves per SIMD (the plain tile order is faster)"
+                best = plain_best
         setup_s += time.perf_counter() - t1
         plan_info = dict(plan_info or {}, occupancy={"waves_per_simd": occupancy["waves_per_simd"],
                                                      "probe_ms": {str(k): round(v, 3) for k, v in best.items()},
                                                      "agreed": "max over ranks" if world > 1 else "single rank"})
+    args.lane_map_np = lane_slots.cpu().numpy() if lane_slots is not None else None
     args.occupancy_chosen = occupancy["waves_per_simd"] or 5
 
     if args.pmc_child:  # under rocprofv3 --pmc: a warm-up and two frames of the production kernel
@@ -703,6 +730,11 @@ def run(args):
     gathered_ev = [torch.cuda.Event(), torch.cuda.Event()]  # the gather that last read bufs[j]
     gather_pending = [False, False]
 
+    # per-frame gather + unshard time: HIP events on comm_stream around rt_gather_shards and (rank 0)
+    # rt_unshard_tiles; the host clock around the synchronous gloo rehearsal gather
+    gev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_total)]
+    gather_host_ms = [0.0] * n_total
+
     def step(i):
         cur, prev = bufs[i & 1], bufs[(i + 1) & 1]
         if comm is not None and gather_pending[i & 1]:
@@ -713,15 +745,20 @@ def run(args):
         if comm is not None:
             rendered.record(stream)
             comm_stream.wait_event(rendered)
+            gev[i][0].record(comm_stream)
             comm.gather(cur, recv_bytes[rank], gathered, cur.numel() * 4, recv_bytes, 0, comm_stream)
             if rank == 0:
                 rt.unshard_tiles(frame, W, H, gathered, lists_dev, stream=comm_stream)
+            gev[i][1].record(comm_stream)
             gathered_ev[i & 1].record(comm_stream)
             gather_pending[i & 1] = True
         elif sharded:
+            th = time.perf_counter()
             got = rt.sharding.gather_shards(cur, rank, world, out=gathered)
             if rank == 0:
                 rt.unshard_tiles(frame, W, H, got, lists_dev)
+                torch.cuda.synchronize()
+            gather_host_ms[i] = (time.perf_counter() - th) * 1e3
 
     wd.phase = "warm-up frames"
     for i in range(args.warmup):
@@ -741,6 +778,7 @@ def run(args):
     elapsed = time.perf_counter() - t_start
 
     wd.phase = "report"
+    exit_code = 0
     segs = int(seg_counter.item())
     kern_ms = [ev[i][0].elapsed_time(ev[i][1]) for i in range(args.warmup, n_total)]
     kern_avg_s = float(np.mean(kern_ms)) / 1e3
@@ -759,6 +797,22 @@ def run(args):
         rank_kernel_ms = km.cpu().tolist()
     else:
         segs_total = segs
+    gather_info = None
+    if sharded:
+        # this rank's gather (+ unshard on rank 0) per timed frame; the line reports rank 0's and the
+        # slowest rank's mean
+        if comm is not None:
+            g_ms = [gev[i][0].elapsed_time(gev[i][1]) for i in range(args.warmup, n_total)]
+        else:
+            g_ms = gather_host_ms[args.warmup:n_total]
+        gm = torch.tensor([float(np.mean(g_ms)), float(np.max(g_ms))], dtype=torch.float64, device=cdev)
+        gmax = gm.clone()
+        dist.all_reduce(gmax, op=dist.ReduceOp.MAX)
+        gather_info = {"gather_ms": round(float(np.mean(g_ms)), 4), "gather_ms_max_frame": round(float(np.max(g_ms)), 4),
+                       "gather_ms_slowest_rank": round(float(gmax[0].item()), 4),
+                       "clock": "HIP events on the gather stream (rt_gather_shards + rt_unshard_tiles on rank 0)"
+                       if comm is not None else "host clock around the synchronous gather + unshard (rehearsal)",
+                       "overlapped_with_next_frame": comm is not None}
 
     seg_per_launch = segs / args.steps
     bytes_per_launch = bytes0 * (seg_per_launch / max(1, int(stats0[0])))
@@ -804,16 +858,24 @@ def run(args):
                                   tiles_per_rank=[int(c) for c in counts] if sharded else None)
         if gather_kind:
             result["gather"] = gather_kind
+            result.update(gather_info)
         if not finite:  # (y, x) of non-finite pixels; the reference arithmetic can produce them too
             result["nonfinite_pixels"] = bad[:8].tolist()
         if args.foreign:
             result["config"]["scene_path"] = "foreign GPUScene (fingerprint-gated private mirror)"
         if args.check:
+            t_chk = time.perf_counter()
             result["check_equal"] = check_unsharded(rt, scene_name, W, H, SPP, BOUNCES, n_total, final)
+            result["check"] = {"frames": n_total, "s": round(time.perf_counter() - t_chk, 2),
+                               "against": "the same frames rendered unsharded in plain tile order (no cost order, "
+                                          "no lane map) on this GPU, final surface compared bit for bit"}
         if world == 1 and not args.no_cpu_baseline:
             auto_rows = {"cfg1": 256, "cfg2": 1080, "cfg3": 64, "cfg4": 540, "cfg5": 1080}[args.config]
             result["cpu_baseline"] = cpu_baseline_child(args.config, args.cpu_rows or auto_rows)
         print(json.dumps(result), flush=True)
+        if args.check and not result["check_equal"]:
+            print("bench.py: the timed frame differs from the unsharded plain render", file=sys.stderr, flush=True)
+            exit_code = 3
     if comm is not None:
         torch.cuda.synchronize()
         comm.close()
@@ -821,7 +883,7 @@ def run(args):
         dist.barrier()
         dist.destroy_process_group()
     wd.cancel()
-    return 0
+    return exit_code
 
 
 def foreign_copy(rt, scene):
@@ -908,8 +970,10 @@ def main():
                     help="rt_set_build_options fields, e.g. leaf_tree_min=300,cluster_max=16 (exact-preserving A/B)")
     ap.add_argument("--rank-deadline", type=float, default=480.0,
                     help="N > 1: seconds after which a still-running job is killed whole (0 = none)")
-    ap.add_argument("--check", action="store_true",
-                    help="after timing, rank 0 re-renders the same frames unsharded and compares the final frame")
+    ap.add_argument("--check", dest="check", action="store_true", default=True,
+                    help="(default) after timing, rank 0 re-renders the same frames unsharded, plain tile order, "
+                         "and compares the final frame bit for bit with the timed one (N > 1: the gathered frame)")
+    ap.add_argument("--no-check", dest="check", action="store_false", help="skip the bit-exact check")
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_baseline_child:  # the CPU baseline's own process (see cpu_baseline_child)

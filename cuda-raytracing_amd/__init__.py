@@ -23,9 +23,11 @@ import torch  # imported before the library so librt_hip.so binds to the HIP run
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "librt_hip.so")
+EXP_LIB_PATH = os.path.join(PKG_DIR, "librt_hip_exp.so")  # experimental render paths (A/B + their tests)
 ASSETS_DIR = os.path.join(ROOT_DIR, "assets")
 
 RT_RENDER_STATS = 1
+RT_RENDER_VALIDATE = 16
 TRACERS = {"fast": 0, "ref": 2, "flat": 4, "wavefront": 8}  # rt_render_params.flags
 STAT_NAMES = ("segments", "nodes", "tri_tests", "tri_accepts", "sphere_accepts", "hits", "misses", "cycles_tree_cut",
               "wave_small_iters", "lane_small", "wave_big_tris", "lane_big_tris", "wave_segment_iters",
@@ -88,6 +90,7 @@ SIGNATURES = {
     "rt_render": (_I, [ctypes.POINTER(RenderParams), _P, _P]),
     "rt_foreign_mirror_wait": (_I, [_P]),
     "rt_foreign_last_tracer": (_I, [_P]),
+    "rt_experimental_loaded": (_I, []),
     "rt_init_rng": (_I, [_P, _I, _I, _I, _I, _U32, _P]),
     "rt_shard_tiles": (ctypes.c_int64, [_I, _I, _I, _I]),
     "rt_unshard": (_I, [_P, _U64, _I, _I, _I, _P, ctypes.c_int64, _P]),
@@ -150,6 +153,7 @@ SIGNATURES = {
     "rt_bvh_build_device": (_I, [_P, _U32, _P, _U32, _P, _P, ctypes.POINTER(_U32), ctypes.POINTER(_I), _P]),
     "rt_scene_mirror_info": (_I, [_P, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
     "rt_scene_mirror_copy": (_I, [_P, _P, _P, _P]),
+    "rt_scene_mirror_nodes": (_I, [_P, _P, ctypes.POINTER(_SZ)]),
     "rt_cluster_cull_host": (_I, [_P, _P, ctypes.c_float, _P]),
     "rt_xorwow_jump_matrix": (_I, [_I, ctypes.POINTER(ctypes.c_uint32)]),
     "rt_xorwow_init_host": (None, [_U32, _U64, _P]),
@@ -175,6 +179,25 @@ def lib():
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+_exp_lib = None
+
+
+def load_experimental():
+    """Load librt_hip_exp.so: registers the exact alternatives kept for A/B measurement -- the
+    wavefront tracer, refill, the lone-pixel kernel and the RT_TUNE A/B kernel variants -- with
+    librt_hip.so, whose rt_render refuses them otherwise.  The benchmark's production path never
+    needs it."""
+    global _exp_lib
+    lib()
+    if _exp_lib is None:
+        if not os.path.exists(EXP_LIB_PATH):
+            raise RTError(f"{EXP_LIB_PATH} not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
+        _exp_lib = ctypes.CDLL(EXP_LIB_PATH)
+    if lib().rt_experimental_loaded() != 1:
+        raise RTError("librt_hip_exp.so loaded but its kernels are not registered with librt_hip.so")
+    return _exp_lib
 
 
 def _check(code, what):
@@ -287,6 +310,16 @@ class Scene:
                "rt_scene_mirror_copy")
         return (tris, tree, ltris) if trees else tris
 
+    def mirror_nodes(self):
+        """The traversal's private node array (mirror.h nodes) as (N, 8) float32 (uint32 view for
+        first / count)."""
+        import numpy as np
+        n = ctypes.c_size_t()
+        _check(lib().rt_scene_mirror_nodes(self.handle, None, ctypes.byref(n)), "rt_scene_mirror_nodes")
+        out = np.zeros((n.value, 8), dtype=np.float32)
+        _check(lib().rt_scene_mirror_nodes(self.handle, out.ctypes.data, ctypes.byref(n)), "rt_scene_mirror_nodes")
+        return out
+
     def host_arrays(self):
         """numpy copies of the host arrays: nodes (N,8) f32/u32 view, face indices, vertices, faces."""
         import numpy as np
@@ -345,13 +378,14 @@ def init_rng_states(rng, width, height, seed, shard_index=0, shard_count=1, stre
 def render(scene, surface, last, width, height, spp, bounces, frame_index=0, shard_index=0, shard_count=1,
            out_shard=None, stats=None, segment_counter=None, stream=None, tracer="fast", tile_list=None,
            wave_clock=None, tune=0, lane_slots=None, lane_cost=None, priority_waves=0, refill_lanes=0,
-           waves_per_simd=0, lone_slots=None):
+           waves_per_simd=0, lone_slots=None, validate=False):
     """rt_render: one frame (or one shard of it) on `stream` (default: torch's current stream).
     tile_list: device int32 tensor of tile ids (a row of a sharding.Plan) instead of the
     round-robin deal; wave_clock: device int64 tensor [entries*4] receiving per-wave clocks;
     tune: diagnostic A/B knobs (0 = production); lane_slots: device int32 lane map (rt_lane_plan,
     a multiple of 64 entries); lane_cost: device int32/uint32 [slots] receiving per-pixel work;
-    lone_slots: device int32 slots for the lone-pixel kernel (rt_lone_plan; needs lane_slots)."""
+    lone_slots: device int32 slots for the lone-pixel kernel (rt_lone_plan; needs lane_slots);
+    validate: RT_RENDER_VALIDATE (lone_slots and lane_slots checked disjoint first; synchronises)."""
     p = RenderParams()
     if lone_slots is not None and lone_slots.numel() > 0:
         assert lone_slots.dtype == torch.int32 and lone_slots.is_cuda and lone_slots.dim() == 1
@@ -381,7 +415,7 @@ def render(scene, surface, last, width, height, spp, bounces, frame_index=0, sha
     p.frame_index, p.spp, p.bounces = frame_index, spp, bounces
     p.shard_index, p.shard_count = shard_index, shard_count
     p.out_shard = out_shard.data_ptr() if out_shard is not None else None
-    p.flags = TRACERS[tracer]
+    p.flags = TRACERS[tracer] | (RT_RENDER_VALIDATE if validate else 0)
     if segment_counter is not None:
         p.segment_counter = segment_counter.data_ptr()
     if stats is not None:

@@ -33,8 +33,13 @@ FP_FLAGS = ["-ffp-contract=off", "-fno-fast-math"]
 HIP_CODEGEN_FLAGS = ["-mllvm", "-structurizecfg-skip-uniform-regions=1"]
 HOST_SOURCES = ["scene.cpp", "objload.cpp", "mirror.cpp", "leaftree.cpp", "xorwow.cpp", "image.cpp", "shard.cpp"]
 # the render kernel families compile as separate translation units, in parallel (rt_render.h)
-HIP_SOURCES = ["rt_fast_prod.hip", "rt_fast_timing.hip", "rt_fast_ab.hip", "rt_fast_ab2.hip", "rt_fast_refill.hip",
-               "rt_fast_stats.hip", "rt_ref.hip", "rt_lone.hip", "rt_wavefront.hip", "rt_kernel.hip", "image.hip", "bvh_build.hip", "comm.hip"]
+HIP_SOURCES = ["rt_fast_prod.hip", "rt_fast_timing.hip", "rt_fast_stats.hip", "rt_ref.hip", "rt_kernel.hip", "image.hip",
+               "bvh_build.hip", "comm.hip"]
+# librt_hip_exp.so: the exact alternatives kept for A/B measurement and their parity tests (A/B kernel
+# variants, refill, the lone-pixel kernel, the wavefront tracer); loading it registers them with
+# librt_hip.so (rt_render.h ExperimentalKernels, rt.load_experimental())
+EXP_SOURCES = ["rt_fast_ab.hip", "rt_fast_ab2.hip", "rt_fast_refill.hip", "rt_lone.hip", "rt_wavefront.hip", "rt_exp.hip"]
+EXP_LIB = os.path.join(PKG, "librt_hip_exp.so")
 
 
 def _run(cmd):
@@ -53,33 +58,59 @@ def _deps(dirpath, exts):
     return [os.path.join(dirpath, f) for f in os.listdir(dirpath) if f.endswith(exts)]
 
 
+def _hip_job(src):
+    obj = os.path.join(BUILD, src + ".o")
+    return obj, [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *FP_FLAGS,
+                 "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics", "-fno-slp-vectorize", *HIP_CODEGEN_FLAGS,
+                 "-I", INC, "-I", CSRC, "-c", os.path.join(CSRC, src), "-o", obj]
+
+
+def _compile(jobs, force):
+    """Compile (object, command) jobs in parallel.  An object is rebuilt when its source or any header
+    changed, or when its command line did (the command is recorded next to the object), so flag A/Bs
+    never link a stale object."""
+    headers = _deps(CSRC, (".h",)) + _deps(INC, (".h",))
+
+    def stale(j):
+        obj, cmd = j
+        rec = obj + ".cmd"
+        same_cmd = os.path.exists(rec) and open(rec).read() == " ".join(cmd)
+        return force or not same_cmd or not _newer(obj, [cmd[cmd.index("-c") + 1]] + headers)
+
+    def run(j):
+        _run(j[1])
+        with open(j[0] + ".cmd", "w") as fh:
+            fh.write(" ".join(j[1]))
+
+    from concurrent.futures import ThreadPoolExecutor
+    workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 8))
+    todo = [j for j in jobs if stale(j)]
+    with ThreadPoolExecutor(max_workers=workers) as ex:
+        list(ex.map(run, todo))
+    return bool(todo)
+
+
 def build_product(force=False):
+    """librt_hip.so and the experimental plugin librt_hip_exp.so (linked against it)."""
     os.makedirs(BUILD, exist_ok=True)
-    deps = _deps(CSRC, (".h", ".hip", ".cpp")) + _deps(INC, (".h",)) + [os.path.abspath(__file__)]
-    if not force and _newer(LIB, deps):
-        return LIB
-    jobs = []
-    headers = _deps(CSRC, (".h",)) + _deps(INC, (".h",)) + [os.path.abspath(__file__)]
-    for src in HIP_SOURCES:
-        obj = os.path.join(BUILD, src + ".o")
-        jobs.append((obj, [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *FP_FLAGS,
-                           "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics", "-fno-slp-vectorize", *HIP_CODEGEN_FLAGS,
-                           "-I", INC, "-I", CSRC, "-c", os.path.join(CSRC, src), "-o", obj]))
+    jobs = [_hip_job(src) for src in HIP_SOURCES]
     for src in HOST_SOURCES:
         obj = os.path.join(BUILD, src + ".o")
         jobs.append((obj, ["g++", "-O2", "-std=c++17", "-fPIC", *FP_FLAGS, "-I", INC, "-I", CSRC,
                            "-c", os.path.join(CSRC, src), "-o", obj]))
-    # translation units compile in parallel (the render kernel's dominates)
-    from concurrent.futures import ThreadPoolExecutor
-    workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 8))
-    # an object is rebuilt when its source or any header changed
-    stale = [j for j in jobs if force or not _newer(j[0], [j[1][j[1].index("-c") + 1]] + headers)]
-    with ThreadPoolExecutor(max_workers=workers) as ex:
-        list(ex.map(lambda j: _run(j[1]), stale))
+    exp_jobs = [_hip_job(src) for src in EXP_SOURCES]
+    changed = _compile(jobs + exp_jobs, force)
     objs = [o for o, _ in jobs]
-    tmp = LIB + ".tmp"
-    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-L/opt/rocm/lib", "-lrccl", "-o", tmp])
-    os.replace(tmp, LIB)
+    if changed or not _newer(LIB, objs):
+        tmp = LIB + ".tmp"
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-L/opt/rocm/lib", "-lrccl", "-o", tmp])
+        os.replace(tmp, LIB)
+    eobjs = [o for o, _ in exp_jobs]
+    if changed or not _newer(EXP_LIB, eobjs + [LIB]):
+        tmp = EXP_LIB + ".tmp"
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *eobjs, "-L", PKG, "-l:librt_hip.so",
+              "-Wl,-rpath,$ORIGIN", "-Wl,--no-undefined", "-o", tmp])
+        os.replace(tmp, EXP_LIB)
     return LIB
 
 

@@ -125,6 +125,43 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
     const uint32_t nl = (uint32_t)(out->ltris.size() / 12);
     for (uint32_t r : roots) std::memcpy(&out->tree[(size_t)r * 16 + 12], &nl, 4);
     rt_build_treelets(nodes, node_count, out->treelets);
+    rt_build_private_nodes(nodes, node_count, out->nodes);
+}
+
+// The traversal's private node array (mirror.h nodes): the reference's BVH nodes renumbered so
+// that (1) every sibling pair -- the two children an inner step loads together -- starts on a
+// 64-B boundary (the reference puts the 32-B root first, so half of its pairs straddle two cache
+// lines), and (2) pairs follow the DFS's own order, right child first (main_raytracing.cu:75-76):
+// pair p of node v, then the pair of v's right child, so the next pair a descending ray needs
+// sits in the same 128-B line.  Slot 0 is the root, slot 1 padding, pair p at slots 2 + 2p and
+// 3 + 2p; an inner node's first_index is its left child's slot, a leaf's is unchanged (the
+// triangle range the tris / pair records are indexed by).  Same boxes, same visit order: the
+// traversal's decisions are the reference's.
+void rt_build_private_nodes(const GPUBVHNode* nodes, size_t node_count, std::vector<float>& out) {
+    out.clear();
+    if (node_count == 0) return;
+    std::vector<uint32_t> slot(node_count, ~0u);  // private slot of every reachable node
+    slot[0] = 0;
+    uint32_t pairs = 0;
+    std::vector<uint32_t> st{0u};
+    while (!st.empty()) {  // pre-order, right child first: the order pairs are numbered in
+        const uint32_t v = st.back();
+        st.pop_back();
+        const GPUBVHNode& nd = nodes[v];
+        if (nd.prim_count > 0) continue;
+        const uint32_t l = nd.first_index, r = nd.first_index + 1;
+        slot[l] = 2 + 2 * pairs, slot[r] = 3 + 2 * pairs;
+        pairs++;
+        st.push_back(l);
+        st.push_back(r);  // popped first
+    }
+    out.assign((size_t)(2 + 2 * pairs) * 8, 0.0f);
+    for (size_t v = 0; v < node_count; v++) {
+        if (slot[v] == ~0u) continue;
+        GPUBVHNode nd = nodes[v];
+        if (nd.prim_count == 0) nd.first_index = slot[nd.first_index];
+        std::memcpy(&out[(size_t)slot[v] * 8], &nd, sizeof nd);
+    }
 }
 
 std::vector<float> rt_ltris_device_layout(const std::vector<float>& ltris) {
@@ -224,30 +261,33 @@ void release(Entry& e) {
 }  // namespace
 
 int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owned, uint64_t fingerprint) {
-    const size_t nt = m.tris.size() * 4, np = m.pairs.size() * 4, nk = m.tree.size() * 4, nl = m.ltris.size() * 4,
-                 ns = m.spairs.size() * 4, nf = m.flat.size() * 4, nq = m.treelets.size() * 4;
     const std::vector<float> lt = rt_ltris_device_layout(m.ltris);
-    void* block = nullptr;
-    if (rt_malloc(&block, nt + np + nk + nl + ns + nf + nq + 64) != 0) return -1;
-    char* b = static_cast<char*>(block);
-    const size_t oq = nt + np + nk + nl + ns + nf;
-    if ((nt && rt_memcpy_h2d(b, m.tris.data(), nt) != 0) || (np && rt_memcpy_h2d(b + nt, m.pairs.data(), np) != 0) ||
-        (nk && rt_memcpy_h2d(b + nt + np, m.tree.data(), nk) != 0) ||
-        (nl && rt_memcpy_h2d(b + nt + np + nk, lt.data(), nl) != 0) ||
-        (ns && rt_memcpy_h2d(b + nt + np + nk + nl, m.spairs.data(), ns) != 0) ||
-        (nf && rt_memcpy_h2d(b + nt + np + nk + nl + ns, m.flat.data(), nf) != 0) ||
-        (nq && rt_memcpy_h2d(b + oq, m.treelets.data(), nq) != 0)) {
-        rt_free(block);
-        return -1;
+    // the parts in one block, each starting on a 256-B boundary (pairs of nodes and records on
+    // cache-line boundaries: mirror.h)
+    const std::vector<float>* parts[8] = {&m.nodes, &m.tris, &m.pairs, &m.tree, &lt, &m.spairs, &m.flat, &m.treelets};
+    size_t off[8], total = 0;
+    for (int i = 0; i < 8; i++) {
+        off[i] = total;
+        total += (parts[i]->size() * 4 + 255) & ~(size_t)255;
     }
+    void* block = nullptr;
+    if (rt_malloc(&block, total + 256) != 0) return -1;
+    char* b = static_cast<char*>(block);
+    for (int i = 0; i < 8; i++)
+        if (!parts[i]->empty() && rt_memcpy_h2d(b + off[i], parts[i]->data(), parts[i]->size() * 4) != 0) {
+            rt_free(block);
+            return -1;
+        }
+    auto at = [&](int i) -> const void* { return parts[i]->empty() ? nullptr : b + off[i]; };
     Entry e{s->gpu_bvh_face_indices, s->gpu_vertices, s->gpu_faces, block, {}};
-    e.dev.tris = b;
-    e.dev.pairs = np ? b + nt : nullptr;
-    e.dev.tree = nk ? b + nt + np : nullptr;
-    e.dev.ltris = nl ? b + nt + np + nk : nullptr;
-    e.dev.spairs = ns ? b + nt + np + nk + nl : nullptr;
-    e.dev.flat = nf ? b + nt + np + nk + nl + ns : nullptr;
-    e.dev.treelets = nq ? b + oq : nullptr;
+    e.dev.nodes = at(0);
+    e.dev.tris = b + off[1];
+    e.dev.pairs = at(2);
+    e.dev.tree = at(3);
+    e.dev.ltris = at(4);
+    e.dev.spairs = at(5);
+    e.dev.flat = at(6);
+    e.dev.treelets = at(7);
     e.dev.depth = m.depth;
     e.dev.fast = m.fast;
     e.dev.owned = owned;

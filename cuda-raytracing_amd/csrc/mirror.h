@@ -27,6 +27,13 @@
 //           mask lo, hi, subtree size in slots, frontier) -- X = the leaf's first triangle, or for
 //           a frontier (an inner node whose children were not taken) the treelet rooted at it,
 //           which holds the same node again in its slot 0; unused slots have count = ~0u;
+//  * nodes  the traversal's private copy of the BVH nodes (rt_fast.h reads only this one): the
+//           reference's nodes renumbered so that every sibling pair starts on a 64-B boundary (the
+//           reference's 32-B root shifts half its pairs across two cache lines) and pairs follow the
+//           DFS's right-first pre-order (main_raytracing.cu:75-76), so a descending ray's next pair
+//           often shares the 128-B line of the pair it just tested.  Slot 0 = root, slot 1 padding,
+//           pair p at slots 2 + 2p, 3 + 2p; an inner node's first_index is its left child's slot, a
+//           leaf's is unchanged.  Same boxes and visit order: the same decisions;
 //  * depth  the deepest leaf (sizes the traversal stack) and whether every node bound lies in
 //           the range where the filtered slab test is proven (rt_fast.h).
 #pragma once
@@ -41,6 +48,7 @@ constexpr uint32_t MIRROR_BIG_LEAF = 8;     // leaves above this get pair record
 constexpr uint32_t MIRROR_TREE_LEAF = 1024;  // ... and leaves this large a leaf tree (leaftree.h) instead
 
 struct MirrorHost {
+    std::vector<float> nodes;     // 8 floats per private node (GPUBVHNode layout)
     std::vector<float> tris;      // 12 floats per record
     std::vector<float> pairs;     // 20 floats per pair
     std::vector<float> spairs;    // 20 floats per triangle position (small leaves' pairs)
@@ -62,12 +70,16 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
 // 2n + i), so a load instruction of a cluster's 16 lanes touches 2 cache lines instead of 6.
 std::vector<float> rt_ltris_device_layout(const std::vector<float>& ltris);
 
+// The private node array alone (also called by rt_build_mirror).
+void rt_build_private_nodes(const GPUBVHNode* nodes, size_t node_count, std::vector<float>& out);
+
 // The treelets alone (also called by rt_build_mirror).
 void rt_build_treelets(const GPUBVHNode* nodes, size_t node_count, std::vector<float>& out);
 
 // Registry: device copies of a mirror, keyed by the GPUScene's BVH node pointer and valid
 // while the scene's face_indices / faces / vertices pointers are the ones it was built from.
 struct MirrorDevice {
+    const void* nodes = nullptr;  // private node array (128-B aligned)
     const void* tris = nullptr;
     const void* pairs = nullptr;
     const void* spairs = nullptr;

@@ -23,7 +23,7 @@ struct FlatTri {
 struct RenderArgs {
     const GeometrySphere* spheres;
     const GPUMaterial* materials;
-    const GPUBVHNode* nodes;
+    const GPUBVHNode* nodes;  // traversal kernels: the mirror's private node array (mirror.h); reference tracers: the scene's
     const uint32_t* face_indices;
     const GPUVertex* vertices;
     const GPUFace* faces;
@@ -65,7 +65,8 @@ struct RenderArgs {
     //   4-5 big-leaf mode (launch_fast_t), 7 statistics through the leaf trees, 8 timing frame (phase
     //   clocks), 9-10 occupancy override (1 compiler's choice, 2 = 6, 3 = 7 waves per SIMD),
     //   11 per-wave clock records, 12 no split small steps, 13-15 split threshold, 16-19 XCD run
-    //   length (xcd_block), 26 no lone-ray traversal, 30 per-lane leaf-tree walk, 31 subtree order.
+    //   length (xcd_block), 26 no lone-ray traversal, 27 the reference's node array instead of the
+    //   mirror's private one (rt_kernel.hip), 30 per-lane leaf-tree walk, 31 subtree order.
     uint32_t tune;
 };
 

@@ -1,5 +1,7 @@
 // rt_fast_prod.hip -- the production variants of the render kernel: MODE 17 (split small steps, pair
-// records; scenes without leaf trees) and 21 (the same with leaf trees), at 5 and 6 waves per SIMD.
+// records; scenes without leaf trees) and 21 (the same with leaf trees), each built for 5, 6 and 7 waves
+// per SIMD (rt_fast_body.h render_fast_kernel_w5 / _w6 / _w7; bench.py's occupancy probe picks one --
+// config 2 runs render_fast_kernel_w7<30, false, 17>).
 #include "rt_fast_body.h"
 
 namespace rtk {

@@ -216,6 +216,18 @@ const uint32_t* device_jump_table() {
 // at most depth + 1 entries; 30 entries -- 7.5 KB of LDS per wave -- still fits 5 waves per SIMD and
 // covers the 4-bunny scene's depth 28), then the MODE bits (rt_fast_body.h render_fast_body), then
 // the translation unit that holds that family (rt_render.h).
+std::atomic<const ExperimentalKernels*> g_experimental{nullptr};
+
+// Whether a frame asks for a kernel of librt_hip_exp.so (rt_render.h): the non-split / big-leaf
+// A/B variants (RT_TUNE bits 12, 4-5), refill, the lone-pixel kernel, the wavefront tracer.
+bool needs_experimental(const rt_render_params* p, bool has_tree) {
+    const bool stats = (p->flags & RT_RENDER_STATS) != 0;
+    if ((p->flags & RT_RENDER_TRACER_WAVEFRONT) || p->refill_lanes || p->lone_count > 0) return true;
+    if (stats || p->lane_cost) return false;  // statistics / timing families are in the product
+    const uint32_t mode = (p->tune >> 4) & 3u;
+    return (p->tune & 4096u) != 0 || (!has_tree && (mode == 2u || mode == 3u));
+}
+
 hipError_t launch_fast(const RenderArgs& args, int waves, int depth, bool stats, hipStream_t s) {
     const int stack = (depth >= 0 && depth + 2 <= 30) ? 30 : (depth >= 0 && depth + 2 <= 40) ? 40 : 64;
     // statistics: the reference's work on scalar records (RT_TUNE bit 7: through the leaf trees);
@@ -230,14 +242,26 @@ hipError_t launch_fast(const RenderArgs& args, int waves, int depth, bool stats,
     // cooperative rounds (MODE 1, measured best); leaf trees compiled in only for scenes that have
     // them (MODE bit 2); A/B: RT_TUNE bits 4-5 = 2 scalar only, 3 pairs everywhere.
     const bool split = (args.tune & 4096u) == 0;
-    if (args.queue_head) return launch_fast_refill(stack, args.tree ? 85 : 81, args, waves, s);  // refill: own variants
-    if (args.tree) return split ? launch_fast_prod(stack, 21, args, waves, s) : launch_fast_ab(stack, 5, args, waves, s);
+    const ExperimentalKernels* x = g_experimental.load();  // rt_render refused these frames without it
+    if (args.queue_head) return x ? x->fast_refill(stack, args.tree ? 85 : 81, args, waves, s) : hipErrorNotSupported;
+    if (args.tree) {
+        if (split) return launch_fast_prod(stack, 21, args, waves, s);
+        return x ? x->fast_ab(stack, 5, args, waves, s) : hipErrorNotSupported;
+    }
     const uint32_t mode = (args.tune >> 4) & 3u;
-    if (mode == 2) return launch_fast_ab(stack, 2, args, waves, s);
-    if (mode == 3) return launch_fast_ab(stack, 0, args, waves, s);
-    return split ? launch_fast_prod(stack, 17, args, waves, s) : launch_fast_ab(stack, 1, args, waves, s);
+    if (split && mode < 2) return launch_fast_prod(stack, 17, args, waves, s);
+    if (!x) return hipErrorNotSupported;
+    if (mode == 2) return x->fast_ab(stack, 2, args, waves, s);
+    if (mode == 3) return x->fast_ab(stack, 0, args, waves, s);
+    return x->fast_ab(stack, 1, args, waves, s);
 }
 
+}  // namespace
+
+void rtk::register_experimental_kernels(const rtk::ExperimentalKernels* k) { g_experimental.store(k); }
+const rtk::ExperimentalKernels* rtk::experimental_kernels() { return g_experimental.load(); }
+
+namespace {
 // Per-(device, stream) side stream of the lone-pixel kernel and its fork / join events.
 struct LoneStreams {
     hipStream_t side = nullptr;
@@ -423,28 +447,28 @@ void upload_mirror(ForeignBuild* b) {
         rt_build_mirror(nodes, b->bytes[0] / sizeof(GPUBVHNode), fi, b->bytes[1] / 4, faces, b->bytes[2] / sizeof(GPUFace),
                         verts, b->bytes[3] / sizeof(GPUVertex), &mh);
         const std::vector<float> lt = rt_ltris_device_layout(mh.ltris);
-        const std::vector<float>* parts[7] = {&mh.tris, &mh.pairs, &mh.tree, &lt, &mh.spairs, &mh.flat, &mh.treelets};
-        size_t total = 64;
-        for (auto* v : parts) total += v->size() * 4;
+        const std::vector<float>* parts[8] = {&mh.tris, &mh.pairs, &mh.tree, &lt, &mh.spairs, &mh.flat, &mh.treelets, &mh.nodes};
+        size_t total = 256;  // each part on a 256-B boundary (mirror.h: cache-line aligned pairs)
+        for (auto* v : parts) total += (v->size() * 4 + 255) & ~(size_t)255;
         hipStream_t st;
         if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) throw std::runtime_error("stream");
         void* block = nullptr;
         if (hipMallocAsync(&block, total, st) != hipSuccess) throw std::runtime_error("mirror allocation failed");
         char* p = static_cast<char*>(block);
-        const void* where[7];
-        for (int i = 0; i < 7; i++) {
+        const void* where[8];
+        for (int i = 0; i < 8; i++) {
             const size_t nb = parts[i]->size() * 4;
             where[i] = nb ? p : nullptr;
             if (nb && hipMemcpyAsync(p, parts[i]->data(), nb, hipMemcpyHostToDevice, st) != hipSuccess)
                 throw std::runtime_error("mirror upload failed");
-            p += nb;
+            p += (nb + 255) & ~(size_t)255;
         }
         const hipError_t e = hipStreamSynchronize(st);  // this worker thread only
         hipStreamDestroy(st);
         if (e != hipSuccess) throw std::runtime_error("mirror upload failed");
         b->block = block;
         b->dev.tris = where[0], b->dev.pairs = where[1], b->dev.tree = where[2], b->dev.ltris = where[3];
-        b->dev.spairs = where[4], b->dev.flat = where[5], b->dev.treelets = where[6];
+        b->dev.spairs = where[4], b->dev.flat = where[5], b->dev.treelets = where[6], b->dev.nodes = where[7];
         b->dev.depth = mh.depth, b->dev.fast = mh.fast, b->dev.owned = false, b->dev.fingerprint = b->fingerprint;
         b->state = 2;
     } catch (const std::exception& e) {
@@ -593,8 +617,54 @@ extern "C" int rt_foreign_mirror_wait(const GPUScene* scene) {
     return fe->have ? 0 : set_error("rt_foreign_mirror_wait: no mirror");
 }
 
-// Per-configuration wave-cost history for the priority scheme in render_fast_body: one uint32
-// per workgroup and three rotating uint64 sums, kept per (device, frame size, shard).
+// RT_RENDER_VALIDATE: lone_slots and lane_slots must be disjoint (a slot in both is rendered twice
+// at once into the same RNG state and pixel).  Marks the lone slots in a bitmap, then counts lane
+// entries that hit a mark or lie outside [0, slots) (< 0 = idle lane, allowed).
+__global__ __launch_bounds__(BLOCK) void mark_slots_kernel(const int32_t* list, long long n, long long slots,
+                                                           uint32_t* bits, unsigned int* bad) {
+    const long long i = (long long)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const int32_t v = list[i];
+    if (v < 0 || v >= slots) {
+        atomicAdd(bad, 1u);
+        return;
+    }
+    if (atomicOr(bits + (v >> 5), 1u << (v & 31)) & (1u << (v & 31))) atomicAdd(bad, 1u);  // listed twice
+}
+__global__ __launch_bounds__(BLOCK) void check_lanes_kernel(const int32_t* lanes, long long n, long long slots,
+                                                            const uint32_t* bits, unsigned int* bad) {
+    const long long i = (long long)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const int32_t v = lanes[i];
+    if (v < 0) return;
+    if (v >= slots || (bits[v >> 5] >> (v & 31) & 1u)) atomicAdd(bad, 1u);
+}
+
+static int validate_lone(const int32_t* lone, long long nl, const int32_t* lanes, long long nm, long long slots,
+                         hipStream_t s) {
+    const size_t words = (size_t)(slots + 31) / 32;
+    uint32_t* bits = nullptr;
+    unsigned int* bad = nullptr;
+    if (hipMallocAsync((void**)&bits, words * 4 + 8, s) != hipSuccess) return set_error("rt_render: validate allocation");
+    bad = reinterpret_cast<unsigned int*>(bits + words);
+    unsigned int h[2] = {0, 0};
+    int rc = 0;
+    if (hipMemsetAsync(bits, 0, words * 4 + 8, s) != hipSuccess) rc = set_error("rt_render: validate memset");
+    if (!rc) {
+        hipLaunchKernelGGL(mark_slots_kernel, dim3((unsigned)((nl + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, lone, nl, slots, bits, bad);
+        hipLaunchKernelGGL(check_lanes_kernel, dim3((unsigned)((nm + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, lanes, nm, slots, bits,
+                           bad + 1);
+        if (hipMemcpyAsync(h, bad, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+            rc = set_error("rt_render: validate read-back");
+    }
+    (void)hipFreeAsync(bits, s);
+    if (rc) return rc;
+    if (h[0]) return set_error("rt_render: RT_RENDER_VALIDATE: " + std::to_string(h[0]) + " lone_slots entries out of range or repeated");
+    if (h[1]) return set_error("rt_render: RT_RENDER_VALIDATE: " + std::to_string(h[1]) +
+                               " lane_slots entries are out of range or also in lone_slots");
+    return 0;
+}
+
 extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void* stream) {
     if (!p || !scene) return set_error("rt_render: null argument");
     if (p->width <= 0 || p->height <= 0 || p->spp <= 0 || p->bounces < 0)
@@ -714,6 +784,10 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     // its pixel state packs the sample count in 16 bits and the bounce in 8; a generation per segment
     if (want_wf && (p->spp > 65535 || p->bounces > 255 || (int64_t)p->spp * p->bounces > 65536))
         return set_error("rt_render: the wavefront tracer needs spp <= 65535, bounces <= 255, spp x bounces <= 65536");
+    if (!g_experimental.load() && needs_experimental(p, a.tree != nullptr))
+        return set_error("rt_render: this frame asks for an experimental render path (wavefront tracer, refill, lone-pixel "
+                         "kernel or an RT_TUNE A/B variant), which lives in librt_hip_exp.so -- load it first "
+                         "(rt.load_experimental())");
     const bool lone = p->lone_count > 0;
     if (p->lone_count < 0 || p->lone_count > (int64_t)1 << 28 || (lone && !p->lone_slots))
         return set_error("rt_render: lone_count must be in [0, 2^28] with lone_slots");
@@ -723,16 +797,24 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     if (lone && (!mir.treelets || depth < 0 || depth > 75))
         return set_error("rt_render: lone_slots need the scene's treelets (a BVH of depth <= 75 with an inner root)");
     if (lone && bytes_from(p->lone_slots) < (size_t)p->lone_count * 4) return set_error("rt_render: lone_slots too small");
+    if ((p->flags & RT_RENDER_VALIDATE) && lone && validate_lone(p->lone_slots, p->lone_count, p->lane_slots,
+                                                                  p->lane_slot_count, a.slot_count, s) != 0)
+        return 1;
     if (p->refill_lanes) {  // the queue counter, zeroed on the launch stream
         a.queue_head = queue_counter(s);
         if (!a.queue_head) return set_error("rt_render: cannot allocate the refill queue counter");
         if (check(hipMemsetAsync(a.queue_head, 0, sizeof(unsigned long long), s), "hipMemsetAsync") != 0) return 1;
     }
     a.scene_fast = scene_fast ? 1 : 0;
+    // the traversal kernels read the mirror's private node array (mirror.h: 64-B aligned sibling
+    // pairs in right-first pre-order; RT_TUNE bit 27: the reference's array instead, A/B); the
+    // reference-layout tracers keep the reference's
+    RenderArgs fa = a;
+    if (mir.nodes && (a.tune & (1u << 27)) == 0) fa.nodes = (const GPUBVHNode*)mir.nodes;
     hipError_t e;
     if (gate) {  // foreign scene with a mirror: exactly one of the two runs, by the frame's fingerprint
         a.gate = gate, a.gate_value = 1;
-        e = want_flat ? launch_ref_tracer(true, a, tiles * 4, depth, stats, s) : launch_fast(a, waves, depth, stats, s);
+        e = want_flat ? launch_ref_tracer(true, a, tiles * 4, depth, stats, s) : launch_fast(fa, waves, depth, stats, s);
         if (e == hipSuccess) {
             RenderArgs r = a;
             r.tris = nullptr, r.gate_value = 0;
@@ -743,21 +825,24 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     else if (want_flat)
         e = launch_ref_tracer(true, a, tiles * 4, depth, stats, s);
     else if (want_wf)
-        e = launch_wavefront(a, depth, s);
+        e = g_experimental.load()->wavefront(fa, depth, s);
     else if (lone) {
         // the lone-pixel kernel on a side stream forked from and joined back into the caller's
         LoneStreams* ls = lone_streams(s);
         if (!ls) return set_error("rt_render: cannot create the lone-pixel stream");
         if (check(hipEventRecord(ls->fork, s), "hipEventRecord") || check(hipStreamWaitEvent(ls->side, ls->fork, 0), "hipStreamWaitEvent"))
             return 1;
-        e = launch_lone(a, p->lone_slots, (int)p->lone_count, mir.treelets, ls->side);
-        if (e == hipSuccess) e = launch_fast(a, waves, depth, stats, s);
+        e = g_experimental.load()->lone(a, p->lone_slots, (int)p->lone_count, mir.treelets, ls->side);
+        if (e == hipSuccess) e = launch_fast(fa, waves, depth, stats, s);
         if (check(hipEventRecord(ls->join, ls->side), "hipEventRecord") || check(hipStreamWaitEvent(s, ls->join, 0), "hipStreamWaitEvent"))
             return 1;
     } else
-        e = launch_fast(a, waves, depth, stats, s);
+        e = launch_fast(fa, waves, depth, stats, s);
     return check(e, "render_kernel launch");
 }
+
+// 1 when librt_hip_exp.so's render paths are registered (rt_render.h ExperimentalKernels).
+extern "C" int rt_experimental_loaded() { return rtk::experimental_kernels() ? 1 : 0; }
 
 extern "C" int rt_init_rng(void* states, int width, int height, int shard_index, int shard_count, uint32_t seed,
                            void* stream) {

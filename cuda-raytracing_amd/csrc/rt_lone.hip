@@ -231,13 +231,22 @@ __global__ __launch_bounds__(WAVE) void render_lone_kernel(RenderArgs a, const i
             Hit h;
             h.best = 1e30f, h.kind = 0, h.id = 0, h.bx = h.by = 0.0f;
             {
-                float dist = 0.0f;
-                bool hit = false;
-                if ((int)lane < a.sphere_count) {
-                    const GeometrySphere& sp = a.spheres[lane];
-                    hit = rtd::intersect_sphere(ro, nd, ld3(sp.position), sp.radius * sp.radius, &dist);
+                // lane l tests spheres l, l + 64, ... keeping its first strictly closer one (the
+                // sequential loop's rule within its own stride); the (distance, index) minimum over
+                // the lanes is then the sequential loop's result
+                float dist = 1e30f;
+                uint32_t idx = 0xffffffffu;
+                bool nan = false;
+                for (int i = (int)lane; i < a.sphere_count; i += WAVE) {
+                    const GeometrySphere& sp = a.spheres[i];
+                    float d;
+                    if (rtd::intersect_sphere(ro, nd, ld3(sp.position), sp.radius * sp.radius, &d)) {
+                        nan = nan || !(d == d);
+                        if (d < dist) dist = d, idx = (uint32_t)i;
+                    }
                 }
-                if (__ballot(hit && !(dist == dist))) {  // a NaN distance: the sequential loop
+                const bool hit = idx != 0xffffffffu;
+                if (__ballot(nan)) {  // a NaN distance: the sequential loop
                     for (int i = 0; i < a.sphere_count; i++) {
                         const GeometrySphere& sp = a.spheres[i];
                         float d2;
@@ -250,7 +259,7 @@ __global__ __launch_bounds__(WAVE) void render_lone_kernel(RenderArgs a, const i
                     const bool cand = hit && dist < 1e30f;  // dist > eps > 0: its bits order like the value
                     const uint32_t mk = rtfast::__ockl_wfred_min_u32(cand ? __float_as_uint(dist) : 0xffffffffu);
                     if (mk != 0xffffffffu) {
-                        const uint32_t mi = rtfast::__ockl_wfred_min_u32(cand && __float_as_uint(dist) == mk ? lane : 0xffffffffu);
+                        const uint32_t mi = rtfast::__ockl_wfred_min_u32(cand && __float_as_uint(dist) == mk ? idx : 0xffffffffu);
                         h.best = __uint_as_float(mk), h.kind = 1, h.id = mi;
                     }
                 }

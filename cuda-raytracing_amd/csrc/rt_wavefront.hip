@@ -339,15 +339,17 @@ __global__ __launch_bounds__(WAVE) void wf_trace_kernel(RenderArgs a, WfBuf b, i
     wf_trace_body<STACK, MODE>(a, b, g);
 }
 
-// Per-device buffers, grown to the largest lane order rendered so far.
+// Per-(device, stream) buffers, grown to the largest lane order rendered so far: frames queued on
+// different streams of one device each have their own pixel state and queues (a frame reuses its
+// stream's block only after the previous frame on that stream, by stream order).
 struct WfCache {
     WfBuf b{};
     size_t bytes = 0;
 };
 
-hipError_t wf_buffers(long long P, int W, int gens, WfBuf* out) {
+hipError_t wf_buffers(long long P, int W, int gens, hipStream_t s, WfBuf* out) {
     static std::mutex mu;
-    static std::map<int, WfCache> per_device;
+    static std::map<std::pair<int, hipStream_t>, WfCache> per_stream;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
@@ -355,7 +357,7 @@ hipError_t wf_buffers(long long P, int W, int gens, WfBuf* out) {
     const size_t L = (size_t)W * C;
     const size_t need = (size_t)P * 112 + L * 56 + (size_t)(2 * gens + 3) * W * 4;
     std::lock_guard<std::mutex> lock(mu);
-    WfCache& wc = per_device[dev];
+    WfCache& wc = per_stream[std::make_pair(dev, s)];
     if (wc.bytes < need) {
         if (wc.b.pst) (void)hipFree(wc.b.pst);
         wc = WfCache{};
@@ -400,7 +402,7 @@ hipError_t launch_wavefront(const RenderArgs& a, int depth, hipStream_t s) {
     // regions over the waves as they finish; measured 29.4 / 29.9 / 31.6 / 32.4 ms for v = 0-3)
     W <<= (a.tune >> 16) & 3u;
     WfBuf b;
-    hipError_t e = wf_buffers(P, W, gens, &b);
+    hipError_t e = wf_buffers(P, W, gens, s, &b);
     if (e != hipSuccess) return e;
     for (int g = 0; g <= gens; g++) {
         hipLaunchKernelGGL(wf_shade_kernel, dim3(b.W), dim3(WAVE), 0, s, a, b, g);

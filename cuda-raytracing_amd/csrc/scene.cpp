@@ -708,6 +708,13 @@ int rt_scene_mirror_copy(rt_scene* s, float* tris, float* tree, float* tree_tris
     std::copy(m.ltris.begin(), m.ltris.end(), tree_tris);
     return 0;
 }
+int rt_scene_mirror_nodes(rt_scene* s, GPUBVHNode* nodes, size_t* count) {
+    MirrorHost m;
+    if (host_mirror(s, &m) != 0) return -1;
+    *count = m.nodes.size() / 8;
+    if (nodes) std::memcpy(nodes, m.nodes.data(), m.nodes.size() * 4);
+    return 0;
+}
 void rt_scene_build(rt_scene* s) { s->scene.BuildHost(); }
 void rt_scene_camera(const rt_scene* s, GPUCamera* out) {
     *out = static_cast<const GPUCamera&>(const_cast<Scene&>(s->scene).GetCamera());

@@ -190,7 +190,7 @@ typedef struct rt_render_params {
     /* With a lane map: the first priority_waves waves (rt_lane_plan's long waves) issue at raised
      * wave priority, so the frame's serial tail does not queue behind the short waves. */
     int64_t priority_waves;
-    /* Refill (production tracer): 0 = off.  n in [1, 64]: the launch holds only as many waves as
+    /* Refill (production tracer; needs librt_hip_exp.so, rt_experimental_loaded): 0 = off.  n in [1, 64]: the launch holds only as many waves as
      * the GPU runs at once; the rest of the lane order (the lane map, or the sub-tile waves) is a
      * queue, and a wave takes the next n entries as soon as n of its lanes have finished their
      * pixels (waves that start less than half full keep their lanes to themselves). */
@@ -203,12 +203,14 @@ typedef struct rt_render_params {
      * wave reserves 160 KB / (4 x cap) of its CU's LDS): fewer co-resident waves for the
      * latency-bound long waves of a strong-scaled shard.  Any other value is an error. */
     int32_t waves_per_simd;
-    /* Lone pixels (production tracer; rt_lone.hip): DEVICE int32 slots (the lane_slots numbering)
-     * that the lone-pixel kernel renders one per wave -- all 64 lanes on the pixel's one ray, the BVH
-     * read as treelets -- concurrently with the production kernel on a second stream joined back
-     * into `stream`.  Requires lane_slots, which must not hold these slots (rt_lone_plan picks them
-     * and marks them for rt_lane_plan).  Bit-identical pixels either way; it shortens the chains
-     * of a strong-scaled frame's costliest pixels.  lone_count 0 = none. */
+    /* Lone pixels (production tracer; rt_lone.hip, needs librt_hip_exp.so): DEVICE int32 slots (the
+     * lane_slots numbering) that the lone-pixel kernel renders one per wave -- all 64 lanes on the
+     * pixel's one ray, the BVH read as treelets -- concurrently with the production kernel on a second
+     * stream joined back into `stream`.  Requires lane_slots, which must not hold these slots
+     * (rt_lone_plan picks them and marks them for rt_lane_plan): a slot in both lists is rendered twice
+     * at the same time into the same RNG state and pixel -- UNDEFINED results.  RT_RENDER_VALIDATE
+     * checks this (and slot ranges) before launching.  Bit-identical pixels either way; it shortens
+     * the chains of a strong-scaled frame's costliest pixels.  lone_count 0 = none. */
     const int32_t* lone_slots;
     int64_t lone_count;
 } rt_render_params;
@@ -221,11 +223,12 @@ typedef struct rt_render_params {
 #define RT_RENDER_STATS 1          /* count traversal work (slower kernel variant) */
 #define RT_RENDER_TRACER_REF 2     /* force the reference-layout tracer (A/B, tests) */
 #define RT_RENDER_TRACER_FLAT 4    /* force the exact-division flat tracer (A/B, tests) */
-#define RT_RENDER_TRACER_WAVEFRONT 8 /* wavefront tracer: a shade launch and a persistent trace launch
-                                        per segment generation, rays refilled lane by lane (same
-                                        results; rt_scene_upload scenes, no statistics / lane_cost /
-                                        wave_clock / refill / lone frames; one frame at a time per
-                                        device) */
+#define RT_RENDER_TRACER_WAVEFRONT 8 /* wavefront tracer (needs librt_hip_exp.so): a shade launch and a
+                                        persistent trace launch per segment generation, rays refilled
+                                        lane by lane (same results; rt_scene_upload scenes, no
+                                        statistics / lane_cost / wave_clock / refill / lone frames) */
+#define RT_RENDER_VALIDATE 16      /* debug: before launching, check on the device that lone_slots and
+                                      lane_slots are disjoint (synchronises; an error if they are not) */
 
 enum {
     RT_STAT_SEGMENTS = 0,   /* GetRayHit calls */
@@ -268,6 +271,11 @@ int rt_foreign_mirror_wait(const GPUScene* scene);
 /* Foreign scenes, for tests: the tracer of the last frame -- 1 production (mirror matched the
  * frame's fingerprint), 0 reference layout (mismatch), -1 no mirror installed yet.  Synchronises. */
 int rt_foreign_last_tracer(const GPUScene* scene);
+
+/* 1 when librt_hip_exp.so is loaded: its constructor registers the exact alternatives kept for A/B
+ * measurement (wavefront tracer, refill, lone-pixel kernel, RT_TUNE A/B kernel variants) with this
+ * library; rt_render refuses frames that ask for them otherwise.  0 otherwise. */
+int rt_experimental_loaded(void);
 
 /* init_rng for the pixels of one shard: state index s of shard (shard_index, shard_count)
  * of a width x height frame gets curand_init(seed, pixel_id(s), 0).  With shard_count == 1
@@ -469,6 +477,10 @@ int rt_bvh_build_device(const GPUVertex* vertices, uint32_t vertex_count, const 
 int rt_scene_mirror_info(rt_scene* scene, size_t* tri_records, size_t* tree_nodes, size_t* tree_tri_records);
 int rt_scene_mirror_copy(rt_scene* scene, float* tris, float* tree, float* tree_tris);
 int rt_cluster_cull_host(const float origin[3], const float nd[3], float best, const float node[16]);
+/* The traversal's private node array (mirror.h nodes: GPUBVHNode records, sibling pairs 64-B
+   aligned in right-first pre-order), built on the host: *count receives the node count; nodes (may
+   be NULL) receives the records.  0 or -1 with rt_last_error(). */
+int rt_scene_mirror_nodes(rt_scene* scene, GPUBVHNode* nodes, size_t* count);
 
 /* XORWOW jump matrix A^(4^k * 2^67) (k < 32) as 800 uint32 words in rocrand's layout
  * m[i*160 + j*5 + w] (input word i, bit j, output word w).  For tests. */

@@ -57,3 +57,25 @@ def test_shard_tiles():
         counts = [rt.shard_tiles(w, h, r, n) for r in range(n)]
         assert sum(counts) == tiles and max(counts) - min(counts) <= 1
     assert rt.shard_tiles(w, h, 8, 8) == 0
+
+
+def test_experimental_paths_live_in_the_plugin():
+    """librt_hip.so carries only the kernels the production path launches; the exact alternatives
+    kept for A/B measurement (wavefront tracer, refill, lone-pixel kernel, RT_TUNE A/B variants) are in
+    librt_hip_exp.so, whose loading registers them (rt_experimental_loaded).  Checked in a child
+    process so the registration starts from a clean slate."""
+    import subprocess
+    import sys
+
+    code = ("import sys, importlib; sys.path.insert(0, %r); rt = importlib.import_module('cuda-raytracing_amd'); "
+            "a = rt.lib().rt_experimental_loaded(); rt.load_experimental(); "
+            "print(a, rt.lib().rt_experimental_loaded())") % T.ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.split() == ["0", "1"]
+    nm = lambda p: subprocess.run(["nm", "-DC", p], capture_output=True, text=True).stdout
+    rt = T.load_rt()
+    prod, exp = nm(rt.LIB_PATH), nm(rt.EXP_LIB_PATH)
+    for k in ("launch_lone", "launch_wavefront", "launch_fast_refill", "launch_fast_ab"):
+        assert f"rtk::{k}(" not in prod and f"rtk::{k}(" in exp, k
+    assert "rtk::launch_fast_prod(" in prod

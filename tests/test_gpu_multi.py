@@ -21,7 +21,9 @@ pytestmark = pytest.mark.gpu
 def rt():
     assert torch.cuda.is_available(), "GPU tests need a HIP device"
     torch.cuda.set_device(0)
-    return T.load_rt()
+    rt = T.load_rt()
+    rt.load_experimental()  # refill / lone-pixel kernels (librt_hip_exp.so)
+    return rt
 
 
 def scene(rt, w, h, which="bunny"):
@@ -307,6 +309,7 @@ def test_bench_two_ranks_without_launcher(tmp_path):
     assert res["plan"]["kind"].startswith("cost") and sum(res["plan"]["tiles_per_rank"]) == 256
     assert res["plan"]["lanes"]["waves"] >= 4 * 128, "the lane plan is rendered (bench --lanes auto)"
     assert len(res["rank_kernel_ms"]) == 2
+    assert res["gather_ms"] > 0 and res["gather_ms_slowest_rank"] > 0, "per-frame gather time in the line"
 
 
 def test_short_buffers_are_refused(rt):
@@ -388,6 +391,100 @@ def test_lone_pixels_config2_full_frame(rt):
     got = rt.surface_view(a, w).cpu().numpy()
     assert np.array_equal(got.view(np.uint32), full.view(np.uint32))
     assert np.array_equal(rng.cpu().numpy(), rng_full)
+
+
+def test_lone_pixels_many_spheres(rt):
+    """More than 64 spheres (rt_scene_add_sphere has no limit): the lone-pixel kernel walks the
+    spheres in strides of 64 lanes and keeps the (distance, index) minimum, so its lone pixels equal
+    the production kernel's sequential sphere loop (main_raytracing.cu:89-103) bit for bit."""
+    w, h, spp, bounces = 64, 48, 2, 4
+
+    def many(s):
+        m = s.add_material(albedo=(0.6, 0.5, 0.4), roughness=0.3, specular_percent=0.2, specular=(0.9, 0.9, 0.9))
+        for i in range(150):  # a cloud of small spheres in front of the bunny, some overlapping
+            s.add_sphere((8.0 + 1.7 * (i % 15), -10.0 + 1.9 * (i // 15), 6.0 + 0.5 * (i % 7)), 1.1, m)
+
+    def fresh():
+        s = scene(rt, w, h)
+        many(s)
+        return s
+
+    s = fresh()
+    rng = rt.alloc_rng(w * h)
+    rt.init_rng_states(rng, w, h, T.SEED)
+    s.upload(rng.data_ptr())
+    bufs = [rt.alloc_surface(w, h), rt.alloc_surface(w, h)]
+    rt.render(s, bufs[0], bufs[1], w, h, spp, bounces, 0)
+    torch.cuda.synchronize()
+    full, rng_full = rt.surface_view(bufs[0], w).cpu().numpy().copy(), rng.cpu().numpy().copy()
+    assert s.gpu.contents.sphere_count > 64
+    s2 = fresh()
+    tiles = rt.sharding.tiles_total(w, h)
+    mine = torch.arange(tiles, dtype=torch.int32, device="cuda")
+    c = lane_costs(rt, s2, w, h, spp, bounces, mine, 1, 0)
+    lone, marked = rt.lone_plan(c, c.size // 2)
+    m, nlong = rt.lane_plan(marked, 48000.0, 1.0)
+    rng2 = rt.alloc_rng(w * h)
+    rt.init_rng_states(rng2, w, h, T.SEED)
+    s2.upload(rng2.data_ptr())
+    out = [rt.alloc_surface(w, h), rt.alloc_surface(w, h)]
+    rt.render(s2, out[0], out[1], w, h, spp, bounces, 0, tile_list=mine, lane_slots=torch.from_numpy(m).cuda(),
+              priority_waves=nlong, lone_slots=torch.from_numpy(lone).cuda())
+    torch.cuda.synchronize()
+    got = rt.surface_view(out[0], w).cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), full.view(np.uint32))
+    assert np.array_equal(rng2.cpu().numpy(), rng_full)
+
+
+def test_lone_and_lane_overlap_is_caught(rt):
+    """A slot in both lone_slots and lane_slots would be rendered twice at once (undefined results,
+    rt_abi.h); RT_RENDER_VALIDATE finds it on the device before anything is launched."""
+    w, h = 64, 64
+    s = scene(rt, w, h)
+    rng = rt.alloc_rng(w * h)
+    rt.init_rng_states(rng, w, h, T.SEED)
+    s.upload(rng.data_ptr())
+    a, b = rt.alloc_surface(w, h), rt.alloc_surface(w, h)
+    mine = torch.arange(rt.sharding.tiles_total(w, h), dtype=torch.int32, device="cuda")
+    lanes = torch.arange(w * h, dtype=torch.int32, device="cuda")
+    lanes[5] = -1
+    lone = torch.tensor([5], dtype=torch.int32, device="cuda")
+    rt.render(s, a, b, w, h, 1, 2, tile_list=mine, lane_slots=lanes, lone_slots=lone, validate=True)  # disjoint
+    torch.cuda.synchronize()
+    lone_bad = torch.tensor([5, 17], dtype=torch.int32, device="cuda")  # 17 is also a lane's slot
+    with pytest.raises(rt.RTError, match="also in lone_slots"):
+        rt.render(s, a, b, w, h, 1, 2, tile_list=mine, lane_slots=lanes, lone_slots=lone_bad, validate=True)
+    with pytest.raises(rt.RTError, match="lone_slots entries"):
+        rt.render(s, a, b, w, h, 1, 2, tile_list=mine, lane_slots=lanes, validate=True,
+                  lone_slots=torch.tensor([5, 5], dtype=torch.int32, device="cuda"))
+    torch.cuda.synchronize()
+
+
+def test_experimental_paths_need_the_plugin():
+    """Without librt_hip_exp.so, rt_render refuses refill / lone / wavefront / A/B frames with an
+    error naming the plugin, before launching anything (child process: this one has it loaded)."""
+    code = """
+import sys, importlib, torch
+sys.path.insert(0, %r); sys.path.insert(0, %r)
+import rt_testlib as T
+rt = T.load_rt()
+w = h = 32
+s = rt.Scene(); s.setup("bunny"); s.set_viewport(w, h)
+rng = rt.alloc_rng(w * h); rt.init_rng_states(rng, w, h, T.SEED); s.upload(rng.data_ptr())
+a, b = rt.alloc_surface(w, h), rt.alloc_surface(w, h)
+rt.render(s, a, b, w, h, 1, 2)
+n = 0
+for kw in (dict(refill_lanes=8), dict(tracer="wavefront"), dict(tune=4096)):
+    try:
+        rt.render(s, a, b, w, h, 1, 2, **kw)
+    except rt.RTError as e:
+        n += "librt_hip_exp.so" in str(e)
+torch.cuda.synchronize()
+print("refused", n)
+""" % (T.ROOT, os.path.join(T.ROOT, "tests"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "refused 3" in r.stdout, r.stdout
 
 
 def test_lone_misuse_is_refused(rt):

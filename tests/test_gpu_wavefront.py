@@ -16,7 +16,9 @@ pytestmark = pytest.mark.gpu
 def rt():
     assert torch.cuda.is_available(), "GPU tests need a HIP device"
     torch.cuda.set_device(0)
-    return T.load_rt()
+    rt = T.load_rt()
+    rt.load_experimental()  # the wavefront tracer lives in librt_hip_exp.so
+    return rt
 
 
 @pytest.mark.parametrize("spp,bounces", [(1, 1), (4, 6), (8, 6)])

@@ -95,3 +95,39 @@ def test_triangle_mirror_records():
     assert np.array_equal(tris[:, 3:6], v1 - v0)
     assert np.array_equal(tris[:, 6:9], v2 - v0)
     assert np.array_equal(tris[:, 9].view(np.uint32), fi)
+
+
+@pytest.mark.parametrize("which", ["bunny", "bunny4"])
+def test_private_node_array(which):
+    """The traversal's private node array (mirror.h nodes): the reference's tree renumbered, node for
+    node the same boxes and leaf ranges, every sibling pair on a 64-B boundary, pairs numbered in the
+    right-first pre-order of BVHRayHit's DFS (main_raytracing.cu:75-76), so the DFS's visit sequence
+    over the private array equals the reference's node by node."""
+    rt = T.load_rt()
+    s = rt.Scene()
+    s.setup(which)
+    s.build()
+    ref = s.host_arrays()["nodes"].view(np.float32).reshape(-1, 8)
+    refu = ref.view(np.uint32)
+    prv = s.mirror_nodes()
+    prvu = prv.view(np.uint32)
+    # walk both trees in the reference's DFS order (push left, push right, pop right first)
+    st = [(0, 0)]
+    seen, pairs_in_order = 0, []
+    while st:
+        a, b = st.pop()
+        seen += 1
+        assert np.array_equal(ref[a, :6].view(np.uint32), prv[b, :6].view(np.uint32)), (a, b)
+        assert refu[a, 7] == prvu[b, 7]
+        if refu[a, 7] > 0:
+            assert refu[a, 6] == prvu[b, 6], "a leaf keeps its triangle range"
+            continue
+        fa, fb = int(refu[a, 6]), int(prvu[b, 6])
+        assert fb % 2 == 0 and (fb * 32) % 64 == 0, "sibling pairs start on a 64-B boundary"
+        pairs_in_order.append(fb)
+        st.append((fa, fb))
+        st.append((fa + 1, fb + 1))
+    assert seen == prv.shape[0] - 1, "every private slot but the padding is reached once"
+    # the pairs are numbered in the order the DFS first reaches them (right-first pre-order)
+    assert pairs_in_order == sorted(pairs_in_order)
+    assert pairs_in_order[0] == 2 and pairs_in_order[-1] == prv.shape[0] - 2

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--lone", type=lambda x: [int(v) for v in x.split(",") if v], default=[256, 1024])
     args = ap.parse_args()
     rt = G.load_package()
+    rt.load_experimental()  # A/B and lone / wavefront / refill paths (librt_hip_exp.so)
     scene_name, W, H, SPP, BOUNCES, _ = bench.CONFIGS[args.config]
     torch.cuda.set_device(0)
     scene = rt.Scene()

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--config", default="cfg2")
     args = ap.parse_args()
     rt = G.load_package()
+    rt.load_experimental()  # A/B and lone / wavefront / refill paths (librt_hip_exp.so)
     scene_name, W, H, SPP, BOUNCES, _ = bench.CONFIGS[args.config]
     torch.cuda.set_device(0)
     scene = rt.Scene()
@@ -61,6 +62,7 @@ def breakdown(rt, scene, W, H, SPP, BOUNCES, tiles):
 
 if __name__ == "__main__" and os.environ.get("HEAVY_BREAKDOWN"):
     rt = G.load_package()
+    rt.load_experimental()  # A/B and lone / wavefront / refill paths (librt_hip_exp.so)
     scene_name, W, H, SPP, BOUNCES, _ = bench.CONFIGS[os.environ["HEAVY_BREAKDOWN"]]
     scene = rt.Scene()
     scene.setup(scene_name)
@@ -109,6 +111,7 @@ def lane_maps(rt, scene, W, H, SPP, BOUNCES, tile):
 
 if __name__ == "__main__" and os.environ.get("HEAVY_LANES"):
     rt = G.load_package()
+    rt.load_experimental()  # A/B and lone / wavefront / refill paths (librt_hip_exp.so)
     scene_name, W, H, SPP, BOUNCES, _ = bench.CONFIGS[os.environ["HEAVY_LANES"]]
     scene = rt.Scene()
     scene.setup(scene_name)

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--tune", type=lambda x: int(x, 0), default=0)
     args = ap.parse_args()
     rt = G.load_package()
+    rt.load_experimental()  # A/B and lone / wavefront / refill paths (librt_hip_exp.so)
     scene_name, W, H, SPP, BOUNCES, _ = bench.CONFIGS[args.config]
     torch.cuda.set_device(0)
     scene = rt.Scene()

@@ -14,6 +14,8 @@ import __graft_entry__ as G  # noqa: E402
 import bench  # noqa: E402
 
 rt = G.load_package()
+
+rt.load_experimental()  # A/B and lone / wavefront / refill paths (librt_hip_exp.so)
 scene_name, W, H, SPP, BOUNCES, _ = bench.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "cfg2"]
 torch.cuda.set_device(0)
 scene = rt.Scene()

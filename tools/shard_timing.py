@@ -136,6 +136,7 @@ def main():
     TUNE, WPS, SPLIT, LONE_MIN, REFINE, THETA = args.tune, args.wps, args.split, args.lone_min, args.refine, args.theta
     lone_list = [int(x) for x in args.lone.split(",")]
     rt = G.load_package()
+    rt.load_experimental()  # A/B and lone / wavefront / refill paths (librt_hip_exp.so)
     scene_name, W0, H0, SPP, BOUNCES, _ = bench.CONFIGS[args.config]
     torch.cuda.set_device(0)
     res = {"config": args.config, "weak": args.weak, "plans": {}}

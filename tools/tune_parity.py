@@ -12,6 +12,8 @@ import __graft_entry__ as G  # noqa: E402
 import bench  # noqa: E402
 
 rt = G.load_package()
+
+rt.load_experimental()  # A/B and lone / wavefront / refill paths (librt_hip_exp.so)
 tune = int(sys.argv[1], 0)
 torch.cuda.set_device(0)
 for cfg in sys.argv[2:] or ["cfg2"]:

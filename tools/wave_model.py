@@ -1,0 +1,224 @@
+"""Per-wave critical-path model of the strong-scaled frame.
+
+A wave of the production kernel is one serial instruction chain (a lane's samples run back to back,
+main_raytracing.cu:188-193; the wave steps through the union of its lanes' chains).  The model:
+
+    duration of wave w  =  integral of  dt / max(1, k(t) / k0)   until  A(w)  has been consumed,
+
+A(w) = the wave's chain measured ALONE on its SIMD (the 5-wave build capped at one resident wave per
+SIMD by dynamic LDS, rt_render_params.waves_per_simd = 1: its per-wave s_memrealtime clock), k(t) =
+the waves resident on its SIMD at time t, and k0 = the residency at which one SIMD's issue saturates:
+alone, a wave issues a dependent VALU instruction every ~8.2 cycles, and the SIMD issues one every
+~1.8 cycles once ~5 waves share it (profiles/r03a_valu_microbench.txt), so k0 = 8.2 / 1.8 = 4.6 --
+a wave slows by k / k0 once more than k0 waves share its SIMD.  Waves are dispatched in workgroup
+order, wave g to SIMD g mod 1024, up to `slots` per SIMD (7 at the 7-wave build), and a finished wave's
+slot takes the next one.  The shard time is the last finish.
+
+    python tools/wave_model.py --measure --ns 1,2,4,8 --out gpurun_out/wave_model.npz   (GPU box)
+    python tools/wave_model.py --model profiles/r04_wave_model.npz                        (anywhere)
+
+--measure renders each rank's shard of the bench's cost plan with the bench's refined lane map
+(rt_lane_plan + 5 rounds of rt_lane_refine, theta 0.85) and records over the same 3 frames: the shard
+time at 7 waves per SIMD (HIP events), every wave's clock at 7 waves per SIMD, and every wave's clock
+alone (cap 1).
+"""
+import argparse
+import heapq
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+SIMDS = 1024
+CLOCK_HZ = 100e6  # wave_clock ticks (s_memrealtime)
+
+
+def simulate(alone_ms, k0, slots, order=None):
+    """Processor-sharing simulation of one launch: `alone_ms[g]` = wave g's chain alone (ms), waves
+    dispatched in order g = 0, 1, ... to SIMD g mod SIMDS while slots last, then into freed slots.
+    Returns (finish time of every wave, the SIMD each ran on)."""
+    n = len(alone_ms)
+    order = np.arange(n) if order is None else order
+    rem = np.asarray(alone_ms, dtype=np.float64).copy()
+    finish = np.zeros(n)
+    simd_of = np.full(n, -1)
+    resident = [[] for _ in range(SIMDS)]
+    t_last = np.zeros(SIMDS)  # time of the SIMD's last update
+    nxt = 0
+    heap = []  # (predicted finish, simd, version)
+    version = np.zeros(SIMDS, dtype=np.int64)
+
+    def rate(s):
+        return 1.0 / max(1.0, len(resident[s]) / k0)
+
+    def advance(s, t):
+        r = rate(s) if resident[s] else 0.0
+        for w in resident[s]:
+            rem[w] -= (t - t_last[s]) * r
+        t_last[s] = t
+
+    def schedule(s):
+        version[s] += 1
+        if resident[s]:
+            w = min(resident[s], key=lambda x: rem[x])
+            heapq.heappush(heap, (t_last[s] + max(rem[w], 0.0) / rate(s), s, version[s]))
+
+    # initial dispatch: round-robin over the SIMDs, `slots` deep
+    for depth in range(slots):
+        for s in range(SIMDS):
+            if nxt >= n:
+                break
+            g = order[nxt]
+            resident[s].append(g)
+            simd_of[g] = s
+            nxt += 1
+    for s in range(SIMDS):
+        schedule(s)
+    while heap:
+        t, s, v = heapq.heappop(heap)
+        if v != version[s]:
+            continue
+        advance(s, t)
+        done = [w for w in resident[s] if rem[w] <= 1e-12]
+        if not done:  # numerical slack
+            done = [min(resident[s], key=lambda x: rem[x])]
+        for w in done:
+            resident[s].remove(w)
+            finish[w] = t
+            if nxt < n:  # the freed slot takes the next wave in dispatch order
+                g = order[nxt]
+                resident[s].append(g)
+                simd_of[g] = s
+                nxt += 1
+        schedule(s)
+    return finish, simd_of
+
+
+def xcd_order(waves):
+    """Logical wave index of hardware workgroup g (rt_fast_body.h xcd_block, runs of 32 per XCD)."""
+    S = 32
+    full = waves // (8 * S) * (8 * S)
+    g = np.arange(waves)
+    i, x = g >> 3, g & 7
+    lb = np.where(g < full, ((i // S) * 8 + x) * S + i % S, g)
+    return lb
+
+
+def measure(args):
+    import torch
+
+    import __graft_entry__ as G
+    import bench
+    import shard_timing as ST
+
+    rt = G.load_package()
+    scene_name, W, H, SPP, BOUNCES, _ = bench.CONFIGS[args.config]
+    torch.cuda.set_device(0)
+    scene = rt.Scene()
+    scene.setup(scene_name)
+    scene.set_viewport(W, H)
+    cost = ST.probe(rt, scene, W, H, SPP, BOUNCES)
+    ST.REFINE, ST.THETA, ST.WPS = args.refine, args.theta, args.wps
+    out = {}
+    for n in map(int, args.ns.split(",")):
+        lists, counts = rt.shard_plan(W, H, n, cost)
+        for r in range(n):
+            mine = torch.from_numpy(lists[r, : counts[r]]).cuda()
+            rng = rt.alloc_rng(mine.numel() * 256)
+            rt.init_rng_tiles(rng, W, H, mine, bench.SEED)
+            scene.upload(rng.data_ptr())
+            lm, nlong, _ = ST.lane_map(rt, scene, W, H, SPP, BOUNCES, mine, rng, (args.units, 1.0))
+            saved = rng.clone()
+            buf = torch.zeros((mine.numel() * 256, 4), dtype=torch.float32, device="cuda")
+            waves = lm.numel() // 64 if lm is not None else mine.numel() * 4
+
+            def frames(clock=True, **kw):
+                ms, acc = [], np.zeros(waves, dtype=np.int64)
+                clk = torch.zeros(waves, dtype=torch.int64, device="cuda")
+                if clock:
+                    kw["wave_clock"] = clk
+                for f in range(3):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    rt.render(scene, None, None, W, H, SPP, BOUNCES, 0, 0, 1, out_shard=buf, tile_list=mine, lane_slots=lm,
+                              **kw)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    ms.append(e0.elapsed_time(e1))
+                    acc += bench.sanitize_wave_clocks(clk.cpu().numpy())[0].astype(np.int64)
+                rng.copy_(saved)
+                return float(np.mean(ms)), acc / 3.0 / CLOCK_HZ * 1e3
+
+            shard_ms = float(np.mean([frames(clock=False, waves_per_simd=args.wps)[0] for _ in range(2)]))
+            full_ms, t_full = frames(waves_per_simd=args.wps)
+            alone_shard_ms, t_alone = frames(waves_per_simd=1)
+            pix = (lm.view(-1, 64) >= 0).sum(1).cpu().numpy() if lm is not None else np.full(waves, 64)
+            key = f"n{n}_r{r}"
+            out[key + "_full"], out[key + "_alone"], out[key + "_pixels"] = t_full, t_alone, pix
+            out[key + "_meta"] = np.array([shard_ms, full_ms, alone_shard_ms, n, r, waves])
+            print(json.dumps({"n": n, "rank": r, "waves": int(waves), "shard_ms": round(shard_ms, 3),
+                              "clocked_frame_ms": round(full_ms, 3), "capped1_frame_ms": round(alone_shard_ms, 3),
+                              "wave_full_ms_max": round(float(t_full.max()), 3), "wave_alone_ms_max": round(float(t_alone.max()), 3),
+                              "sum_alone_ms": round(float(t_alone.sum()), 1)}), flush=True)
+    np.savez_compressed(args.out, **out)
+
+
+def model(args):
+    d = np.load(args.model)
+    keys = sorted({k.rsplit("_", 1)[0] for k in d.files})
+    rows = []
+    for key in keys:
+        meta = d[key + "_meta"]
+        shard_ms, n, r, waves = float(meta[0]), int(meta[3]), int(meta[4]), int(meta[5])
+        alone, full, pix = d[key + "_alone"], d[key + "_full"], d[key + "_pixels"]
+        lb = xcd_order(waves)  # hardware dispatch order g -> logical wave lb
+        fin, simd = simulate(alone, args.k0, args.slots, order=lb)
+        pred = float(fin.max())
+        crit = int(simd[int(np.argmax(fin))])
+        on = np.flatnonzero(simd == crit)
+        rows.append({"n": n, "rank": r, "waves": waves, "measured_ms": round(shard_ms, 3), "model_ms": round(pred, 3),
+                     "err": round(pred / shard_ms - 1, 3),
+                     "critical_simd": {"waves": int(on.size), "alone_ms": [round(float(x), 3) for x in np.sort(alone[on])[::-1]],
+                                       "pixels": [int(pix[w]) for w in on[np.argsort(-alone[on])]]},
+                     "longest_alone_ms": round(float(alone.max()), 3),
+                     "mean_waves_per_simd": round(waves / SIMDS, 2),
+                     "slowdown_measured_p50": round(float(np.median(full / np.maximum(alone, 1e-9))), 3)})
+    by_n = {}
+    for row in rows:
+        by_n.setdefault(row["n"], []).append(row)
+    summary = {str(n): {"measured_ms": max(x["measured_ms"] for x in v), "model_ms": max(x["model_ms"] for x in v)}
+               for n, v in sorted(by_n.items())}
+    for v in summary.values():
+        v["err"] = round(v["model_ms"] / v["measured_ms"] - 1, 3)
+    for row in rows:
+        print(json.dumps(row))
+    print(json.dumps({"k0": args.k0, "slots": args.slots, "per_n_slowest_rank": summary}))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--measure", action="store_true")
+    ap.add_argument("--model", default=None)
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--ns", default="1,2,4,8")
+    ap.add_argument("--refine", type=int, default=5)
+    ap.add_argument("--theta", type=float, default=0.85)
+    ap.add_argument("--units", type=float, default=48000.0)
+    ap.add_argument("--wps", type=int, default=7)
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "wave_model.npz"))
+    ap.add_argument("--k0", type=float, default=8.2 / 1.8)
+    ap.add_argument("--slots", type=int, default=7)
+    args = ap.parse_args()
+    if args.measure:
+        measure(args)
+    if args.model:
+        model(args)
+
+
+if __name__ == "__main__":
+    main()

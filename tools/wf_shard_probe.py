@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--frames", type=int, default=6)
     args = ap.parse_args()
     rt = G.load_package()
+    rt.load_experimental()  # A/B and lone / wavefront / refill paths (librt_hip_exp.so)
     scene_name, W, H, SPP, BOUNCES, _ = bench.CONFIGS[args.config]
     torch.cuda.set_device(0)
     scene = rt.Scene()
