@@ -64,7 +64,8 @@ class GPUMaterial(ctypes.Structure):
 class BuildOptions(ctypes.Structure):
     """rt_build_options (rt_abi.h): exact-preserving speed knobs of the mirror / BVH builders."""
     _fields_ = [("leaf_tree_min", ctypes.c_uint32), ("cut_clusters", ctypes.c_uint32), ("cluster_max", ctypes.c_uint32),
-                ("split_angle", ctypes.c_float), ("bvh_small", ctypes.c_uint32), ("host_bvh", ctypes.c_int32)]
+                ("split_angle", ctypes.c_float), ("bvh_small", ctypes.c_uint32), ("host_bvh", ctypes.c_int32),
+                ("leaf_screens", ctypes.c_int32)]
 
 
 class RenderParams(ctypes.Structure):

@@ -172,8 +172,9 @@ struct Builder {
 
 }  // namespace
 
-uint32_t rt_build_leaf_tree(const float* recs, uint32_t count, const LeafTreeParams& prm, std::vector<float>& nodes,
-                            std::vector<float>& ltris) {
+namespace {
+// corners, normal and edge lengths of the fp32 triangles (double)
+std::vector<Tri> leaf_tris(const float* recs, uint32_t count, double* ext_out) {
     std::vector<Tri> t(count);
     double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
     for (uint32_t j = 0; j < count; j++) {
@@ -195,7 +196,38 @@ uint32_t rt_build_leaf_tree(const float* recs, uint32_t count, const LeafTreePar
         q.nlen = std::sqrt(q.n[0] * q.n[0] + q.n[1] * q.n[1] + q.n[2] * q.n[2]);
         q.el1 = std::max(std::fabs(b[0]) + std::fabs(b[1]) + std::fabs(b[2]), std::fabs(a[0]) + std::fabs(a[1]) + std::fabs(a[2]));
     }
-    const double ext = std::max({hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]});
+    *ext_out = std::max({hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]});
+    return t;
+}
+}  // namespace
+
+bool rt_build_leaf_screen(const float* recs, uint32_t count, const LeafTreeParams& prm, float out[20]) {
+    double ext = 0;
+    const std::vector<Tri> t = leaf_tris(recs, count, &ext);
+    std::vector<uint32_t> big, rest;
+    for (uint32_t j = 0; j < count; j++) (t[j].nlen == 0.0 || t[j].el1 > prm.big_fraction * ext ? big : rest).push_back(j);
+    if (big.size() > kScreenOutliers || rest.empty()) return false;
+    std::vector<float> nodes, ltris;
+    Builder B{t, prm, nodes, ltris};
+    const uint32_t k = B.alloc();
+    B.fill(k, rest, true, ~0u);
+    uint32_t info;
+    std::memcpy(&info, &nodes[15], 4);
+    if (!(info & 1u)) return false;  // the core's cone is too wide: cluster_cull could never prove it
+    std::memcpy(out, nodes.data(), 12 * 4);
+    out[12] = nodes[12];  // sin of the cone
+    const uint32_t nb = (uint32_t)big.size(), none = ~0u, zero = 0;
+    std::memcpy(&out[13], &nb, 4);
+    std::memcpy(&out[14], &zero, 4);
+    std::memcpy(&out[15], &zero, 4);
+    for (uint32_t i = 0; i < kScreenOutliers; i++) std::memcpy(&out[16 + i], i < nb ? &big[i] : &none, 4);
+    return true;
+}
+
+uint32_t rt_build_leaf_tree(const float* recs, uint32_t count, const LeafTreeParams& prm, std::vector<float>& nodes,
+                            std::vector<float>& ltris) {
+    double ext = 0;
+    const std::vector<Tri> t = leaf_tris(recs, count, &ext);
     Builder B{t, prm, nodes, ltris};
     // root: a non-culled node whose children are the big / degenerate triangles one by one (never
     // culled: their bound would be useless) and a tree over the rest

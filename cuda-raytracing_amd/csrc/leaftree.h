@@ -55,6 +55,15 @@ struct LeafTreeParams {
 uint32_t rt_build_leaf_tree(const float* recs, uint32_t count, const LeafTreeParams& prm, std::vector<float>& nodes,
                             std::vector<float>& ltris);
 
+// Screen record of a big leaf (rt_fast.h screen_leaf, mirror.h pf = 3): the leaf's triangles split
+// into at most kScreenOutliers "outliers" (the big / degenerate ones the tree root keeps apart) and a
+// core whose one node record (box, E1, Nmin, normal cone -- the fields cluster_cull reads) proves for a
+// ray that none of the core can pass the fp32 test.  20 floats: K0, K1, K2, (sin, outlier count, 0, 0),
+// (outlier positions in the leaf, ascending; ~0 unused).  Returns false (no record) when the core's
+// cone is too wide to ever cull (cluster_cull needs cos > min_cull_cos) or there are too many outliers.
+constexpr uint32_t kScreenOutliers = 4;
+bool rt_build_leaf_screen(const float* recs, uint32_t count, const LeafTreeParams& prm, float out[20]);
+
 // Appends the flat cluster and cut lists of the tree rooted at `root` to `flat` (16 floats per
 // record) and records their place in the root (see above).
 void rt_build_leaf_flat(std::vector<float>& nodes, uint32_t root, const LeafTreeParams& prm, std::vector<float>& flat);

@@ -53,6 +53,7 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
     out->flat.clear();
     out->depth = 0;
     out->fast = true;
+    out->screens = 0;
     std::vector<uint32_t> big;
     out->spairs.assign(index_count * 20, 0.0f);
     if (node_count == 0) return;
@@ -110,8 +111,19 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
             std::memcpy(&lead[11], &pf, 4);
             continue;
         }
-        po = (uint32_t)(out->pairs.size() / 20);
+        // a screen record right before the pairs when the leaf has one (pf = 3, rt_fast.h screen_leaf)
+        float scr[20];
+        rt_build_options so;
+        rt_get_build_options(&so);
+        LeafTreeParams sp;
+        sp.split_angle = so.split_angle;
         pf = 1;
+        if (so.leaf_screens && rt_build_leaf_screen(&out->tris[(size_t)nd.first_index * 12], nd.prim_count, sp, scr)) {
+            out->pairs.insert(out->pairs.end(), scr, scr + 20);
+            pf = 3;
+            out->screens++;
+        }
+        po = (uint32_t)(out->pairs.size() / 20);
         std::memcpy(&lead[10], &po, 4);
         std::memcpy(&lead[11], &pf, 4);
         for (uint32_t j = 0; j < nd.prim_count; j += 2) {
@@ -290,6 +302,7 @@ int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owne
     e.dev.treelets = at(7);
     e.dev.depth = m.depth;
     e.dev.fast = m.fast;
+    e.dev.screens = m.screens;
     e.dev.owned = owned;
     e.dev.fingerprint = fingerprint;
     std::lock_guard<std::mutex> lock(g_mutex);
@@ -341,6 +354,7 @@ rt_build_options default_options() {
     o.split_angle = (float)p.split_angle;
     o.bvh_small = 16;
     o.host_bvh = 0;
+    o.leaf_screens = 1;
     return o;
 }
 rt_build_options g_options = default_options();
@@ -355,7 +369,8 @@ extern "C" void rt_get_build_options(rt_build_options* out) {
 extern "C" int rt_set_build_options(const rt_build_options* o) {
     const rt_build_options v = o ? *o : default_options();
     if (v.leaf_tree_min < 2 || v.cut_clusters < 1 || v.cut_clusters > 32 || v.cluster_max < 1 || v.cluster_max > kClusterMax ||
-        !(v.split_angle >= 0.0f && v.split_angle < 3.2f) || v.bvh_small < 2 || v.bvh_small > 64 || (v.host_bvh != 0 && v.host_bvh != 1)) {
+        !(v.split_angle >= 0.0f && v.split_angle < 3.2f) || v.bvh_small < 2 || v.bvh_small > 64 || (v.host_bvh != 0 && v.host_bvh != 1) ||
+        (v.leaf_screens != 0 && v.leaf_screens != 1)) {
         rt_internal_set_error("rt_set_build_options: value out of range");
         return 1;
     }

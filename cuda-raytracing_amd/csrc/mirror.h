@@ -11,7 +11,10 @@
 //           two with each component interleaved, 80 B per pair: (v0x_a, v0x_b, v0y_a, v0y_b),
 //           (v0z, e1x), (e1y, e1z), (e2x, e2y), (e2z_a, e2z_b, face_a, face_b) -- the operand
 //           layout of packed fp32 instructions; an odd leaf ends with an all-zero triangle.  The
-//           leaf's first tris record holds po = its first pair, pf = 1 (0 for other leaves);
+//           leaf's first tris record holds po = its first pair, pf = 1 (0 for other leaves), or
+//           pf = 3 when a screen record (leaftree.h rt_build_leaf_screen: the cull record of the
+//           leaf's core and the positions of its few big "outlier" triangles) sits in the 80-B slot
+//           just before the pairs, at po - 1 (rt_fast.h screen_leaf);
 //  * spairs for every leaf of at most BIG triangles, its triangles two by two in the pairs layout,
 //           the pair of triangles (i, i + 1) stored at record i (i = first, first + 2, ...; an
 //           odd leaf ends with an all-zero triangle), so a small leaf needs no index of its own;
@@ -58,6 +61,7 @@ struct MirrorHost {
     std::vector<float> treelets;  // 64 slots x 12 floats per treelet (rt_lone.hip)
     int depth = 0;                // deepest leaf (root = 0) reachable from node 0
     bool fast = true;             // node bounds inside the filtered-slab range (rt_fast.h)
+    int screens = 0;              // big leaves with a screen record (pf = 3)
 };
 
 // Build from host copies of the reference arrays.  node_count / face_count / vertex_count
@@ -89,6 +93,7 @@ struct MirrorDevice {
     const void* treelets = nullptr;
     int depth = -1;
     bool fast = false;
+    int screens = 0;
     bool owned = true;         // built by rt_scene_upload, which forgets it before freeing the arrays
     uint64_t fingerprint = 0;  // foreign scenes: content hash of the arrays it was built from
 };

@@ -55,6 +55,7 @@ struct RenderArgs {
     unsigned long long* stats;
     unsigned long long* seg_counter;
     int scene_fast;  // all node bounds inside the filtered-slab range (rt_fast.h)
+    int screens;     // the mirror has big-leaf screen records (mirror.h pf = 3; rt_fast.h screen_leaf)
     const float4* pairs;  // big leaves' triangles in packed pairs (mirror.h) or null
     const float4* tree;   // leaf trees of huge leaves (leaftree.h) or null
     const float4* ltris;  // their triangle records
@@ -66,7 +67,8 @@ struct RenderArgs {
     //   clocks), 9-10 occupancy override (1 compiler's choice, 2 = 6, 3 = 7 waves per SIMD),
     //   11 per-wave clock records, 12 no split small steps, 13-15 split threshold, 16-19 XCD run
     //   length (xcd_block), 26 no lone-ray traversal, 27 the reference's node array instead of the
-    //   mirror's private one (rt_kernel.hip), 30 per-lane leaf-tree walk, 31 subtree order.
+    //   mirror's private one (rt_kernel.hip), 28 no big-leaf screens, 30 per-lane leaf-tree walk,
+    //   31 subtree order.
     uint32_t tune;
 };
 

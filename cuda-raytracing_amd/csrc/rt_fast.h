@@ -638,8 +638,12 @@ __device__ __forceinline__ void tree_leaf(const float4* tris, const float4* tree
 // Traversal state of one lane between steps: the node (or leaf) it is at and its stack depth.
 struct Trav {
     uint32_t first, count;
-    int sp;
+    int sp;  // stack depth; bit SCREENED: at a big leaf whose screen has run (waiting for the round)
 };
+// Trav::sp flag (screen variants): the lane's big leaf has been screened and it waits for the wave's
+// big-leaf round.  Kept in the depth word rather than in a bool of its own (a per-lane bool lives in a
+// lane mask, and the 6-wave build of the screen variants mis-rendered with one: tools/variant_agree.py).
+constexpr int SCREENED = 1 << 30;
 
 // Cooperative walk of the leaf trees through their flat lists (leaftree.h) for the lanes `m`
 // waiting at tree leaves, one ray at a time: the whole wave screens the cut subtrees (a lane per
@@ -816,12 +820,47 @@ __device__ __forceinline__ bool trav_begin(const float4* nodes4, const Ray& R, c
     return tmax >= tmin && tmin < h.best && tmax > 0.0f;
 }
 
+// A big leaf's screen (mirror.h pf = 3, leaftree.h rt_build_leaf_screen), run by a lane when it
+// reaches the leaf: when cluster_cull proves that none of the leaf's core triangles can pass glm's
+// fp32 test with 0 <= t < closest for this ray, the sequential loop over the leaf
+// (main_raytracing.cu:51-71) can accept only the few outlier triangles (the big ones the core's box
+// leaves out), so the lane tests those, in leaf order, and moves on without waiting for the wave's
+// big-leaf round.  Returns true when the leaf is done that way.
+template <bool STATS, class C>
+__device__ __forceinline__ bool screen_leaf(const float4* tris, const float4* pairs, const Ray& R, Hit& h, const Trav& T,
+                                            C& c) {
+    if (!R.fast || !pairs) return false;
+    const float4 lead = tris[3 * (size_t)T.first + 2];
+    if (__float_as_uint(lead.w) != 3u) return false;
+    const float4* S = pairs + 5 * ((size_t)__float_as_uint(lead.z) - 1);
+    const float4 K0 = S[0], K1 = S[1], K2 = S[2], K3 = S[3];
+    const f3 rnd = rtm::mk(1.0f / R.nd.x, 1.0f / R.nd.y, 1.0f / R.nd.z);
+    if (!cluster_cull(R, rnd, h.best, K0, K1, K2, K3)) return false;
+    const float4 P = S[4];
+    const uint32_t n = __float_as_uint(K3.y);
+    const uint32_t pos[4] = {__float_as_uint(P.x), __float_as_uint(P.y), __float_as_uint(P.z), __float_as_uint(P.w)};
+    for (uint32_t k = 0; k < n && k < 4u; k++) {
+        const size_t i = (size_t)T.first + pos[k];
+        test_triangle<STATS>(R, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], h, c);
+    }
+    return true;
+}
+
 // One small step of a lane at a small leaf or an inner node; false when the traversal is over.
 // (Testing a small leaf in the same step as the inner node that entered it was measured slower:
 // 22.2 vs 20.6 ms, the extra divergence costs more than the saved iterations.)
-template <bool STATS, class S, class C>
+template <bool STATS, bool SCR = false, class S, class C>
 __device__ __forceinline__ bool small_step(const float4* nodes4, const float4* tris, const float4* spairs, const S& stk,
-                                           const Ray& R, Hit& h, Trav& T, C& c) {
+                                           const Ray& R, Hit& h, Trav& T, C& c, const float4* pairs = nullptr) {
+    if constexpr (SCR) {
+        if (T.count > (uint32_t)BIG) {  // a big leaf just reached: its screen, else wait for the round
+            if (!screen_leaf<STATS>(tris, pairs, R, h, T, c)) {
+                T.sp |= SCREENED;
+                return true;
+            }
+            return pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
+        }
+    }
     if (T.count > 0) {
         if (!STATS && spairs) {
             // two triangles per packed pair record (mirror.h spairs), in leaf order
@@ -881,7 +920,7 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
         // the first record of a big leaf says where its pairs are (mirror.h)
         const f4v lead = ((ConstF4)(tris + 3 * (size_t)f0))[2];
         const uint32_t k = (uint32_t)__popcll(big);
-        if (!STATS && (MODE & 3) < 2 && pairs && __float_as_uint(lead.w) == 1u) {
+        if (!STATS && (MODE & 3) < 2 && pairs && (__float_as_uint(lead.w) & 1u)) {
             const float4* lp = pairs + 5 * (size_t)__float_as_uint(lead.z);
             const uint32_t np = (c0 + 1u) / 2u, chunks = (np + 63u) / 64u;
             // cost model (VALU instructions per pair ~40): cooperative ~ k * (40 * chunks + 60),
@@ -1112,6 +1151,8 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                                       const Ray& R, Hit& h, bool live, C& c) {
     Trav T{0, 0, 0};
     bool active = live && trav_begin<STATS>(nodes4, R, h, T, c);
+    // big-leaf screens (screen_leaf, MODE bit 5): split-step variants for scenes that have them
+    constexpr bool scr_on = !STATS && (MODE & 16) != 0 && (MODE & 32) != 0;
     constexpr bool TIMING = (MODE & 8) != 0;
     unsigned long long t0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
     for (;;) {
@@ -1122,16 +1163,18 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
             // of both: 19.8 -> 18.3 ms/frame.  (A three-way split with pops as a third kind, the
             // wave picking the kind with the most lanes per unit of cost, measured the same.)
             const bool inner = active && T.count == 0;
-            const bool leafs = active && T.count > 0 && T.count <= (uint32_t)BIG;
+            const bool leafs = active && T.count > 0 && (T.count <= (uint32_t)BIG || (scr_on && !(T.sp & SCREENED)));
             const unsigned long long mI = __ballot(inner), mL = __ballot(leafs);
             if (mI | mL) {
                 const uint32_t nI = (uint32_t)__popcll(mI), nL = (uint32_t)__popcll(mL);
                 if constexpr (!STATS) {
                     // one lane left in the small phase: the whole wave runs its DFS (lone_traverse),
-                    // when its stack lives in LDS (RT_TUNE bit 26 turns this off)
+                    // when its stack lives in LDS (RT_TUNE bit 26 turns this off); a lane that must
+                    // screen a big leaf first takes an ordinary step
                     if (nI + nL == 1 && (tune & (1u << 26)) == 0) {
                         const int r = __ffsll((long long)(mI | mL)) - 1;
-                        if (__builtin_amdgcn_readlane(T.sp, r) <= S::LDS_ENTRIES) {
+                        if (__builtin_amdgcn_readlane(T.sp, r) <= S::LDS_ENTRIES &&
+                            (!scr_on || (uint32_t)__builtin_amdgcn_readlane((int)T.count, r) <= (uint32_t)BIG)) {
 #ifdef RT_LANE_HIST  // diagnostic build (tools/lane_hist.sh): wave cycles of the lone-lane tails
                             const unsigned long long tl0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
 #endif
@@ -1151,7 +1194,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
 #endif
                 if (!mI || nL * 4u >= nI * (q + 1u)) {
                     if (leafs) {
-                        active = small_step<STATS>(nodes4, tris, spairs, stk, R, h, T, c);
+                        active = small_step<STATS, scr_on>(nodes4, tris, spairs, stk, R, h, T, c, pairs);
                         if (TIMING) c.lane_work++;
                     }
                 } else if (inner) {
@@ -1196,6 +1239,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
         if (big_round<STATS, MODE>(tris, pairs, tree, ltris, flat, scratch, tune, big, active, R, h, T, c)) {
             // a big leaf run alone (cooperative round) costs about as much as 3 small steps
             if (TIMING) c.lane_work += 3;
+            if constexpr (scr_on) T.sp &= ~SCREENED;
             active = pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
         }
         if (TIMING) {

@@ -232,10 +232,12 @@ hipError_t launch_fast(const RenderArgs& args, int waves, int depth, bool stats,
     const int stack = (depth >= 0 && depth + 2 <= 30) ? 30 : (depth >= 0 && depth + 2 <= 40) ? 40 : 64;
     // statistics: the reference's work on scalar records (RT_TUNE bit 7: through the leaf trees);
     // RT_TUNE bit 8: a timing frame of the production kernel instead (phase clocks, no counts)
+    // MODE bit 5: big-leaf screens compiled in, for scenes whose mirror has screen records (mirror.h pf = 3)
+    const int sm = args.screens ? 32 : 0;
     if (stats && (args.tune & 256u))
-        return launch_fast_timing(stack, args.tree ? 29 : (args.tune & 4096u) ? 9 : 25, args, waves, s);
+        return launch_fast_timing(stack, args.tree ? 29 + sm : (args.tune & 4096u) ? 9 : 25 + sm, args, waves, s);
     // per-pixel work (rt_render_params.lane_cost): the timing variant of the production kernel
-    if (!stats && args.lane_cost) return launch_fast_timing(stack, args.tree ? 29 : 25, args, waves, s);
+    if (!stats && args.lane_cost) return launch_fast_timing(stack, (args.tree ? 29 : 25) + sm, args, waves, s);
     if (stats) return launch_fast_stats(stack, (args.tree && (args.tune & 128u)) ? 6 : 2, args, waves, s);
     // MODE bit 4: inner-node and small-leaf steps in separate iterations (rt_fast.h trace); RT_TUNE
     // bit 12 turns it off (A/B).  Big leaves: packed pairs in the shared-leaf loop, scalar records in
@@ -245,11 +247,11 @@ hipError_t launch_fast(const RenderArgs& args, int waves, int depth, bool stats,
     const ExperimentalKernels* x = g_experimental.load();  // rt_render refused these frames without it
     if (args.queue_head) return x ? x->fast_refill(stack, args.tree ? 85 : 81, args, waves, s) : hipErrorNotSupported;
     if (args.tree) {
-        if (split) return launch_fast_prod(stack, 21, args, waves, s);
+        if (split) return launch_fast_prod(stack, 21 + sm, args, waves, s);
         return x ? x->fast_ab(stack, 5, args, waves, s) : hipErrorNotSupported;
     }
     const uint32_t mode = (args.tune >> 4) & 3u;
-    if (split && mode < 2) return launch_fast_prod(stack, 17, args, waves, s);
+    if (split && mode < 2) return launch_fast_prod(stack, 17 + sm, args, waves, s);
     if (!x) return hipErrorNotSupported;
     if (mode == 2) return x->fast_ab(stack, 2, args, waves, s);
     if (mode == 3) return x->fast_ab(stack, 0, args, waves, s);
@@ -470,6 +472,7 @@ void upload_mirror(ForeignBuild* b) {
         b->dev.tris = where[0], b->dev.pairs = where[1], b->dev.tree = where[2], b->dev.ltris = where[3];
         b->dev.spairs = where[4], b->dev.flat = where[5], b->dev.treelets = where[6], b->dev.nodes = where[7];
         b->dev.depth = mh.depth, b->dev.fast = mh.fast, b->dev.owned = false, b->dev.fingerprint = b->fingerprint;
+        b->dev.screens = mh.screens;
         b->state = 2;
     } catch (const std::exception& e) {
         b->error = e.what();
@@ -806,15 +809,21 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
         if (check(hipMemsetAsync(a.queue_head, 0, sizeof(unsigned long long), s), "hipMemsetAsync") != 0) return 1;
     }
     a.scene_fast = scene_fast ? 1 : 0;
+    a.screens = (mir.screens > 0 && (a.tune & (1u << 28)) == 0) ? 1 : 0;  // RT_TUNE bit 28: no big-leaf screens
     // the traversal kernels read the mirror's private node array (mirror.h: 64-B aligned sibling
     // pairs in right-first pre-order; RT_TUNE bit 27: the reference's array instead, A/B); the
     // reference-layout tracers keep the reference's
-    RenderArgs fa = a;
-    if (mir.nodes && (a.tune & (1u << 27)) == 0) fa.nodes = (const GPUBVHNode*)mir.nodes;
+    const GPUBVHNode* const trav_nodes =
+        (mir.nodes && (a.tune & (1u << 27)) == 0) ? (const GPUBVHNode*)mir.nodes : scene->gpu_bvh_nodes;
+    auto trav = [&](const RenderArgs& x) {  // the arguments as they stand at launch, traversal nodes
+        RenderArgs f = x;
+        f.nodes = trav_nodes;
+        return f;
+    };
     hipError_t e;
     if (gate) {  // foreign scene with a mirror: exactly one of the two runs, by the frame's fingerprint
         a.gate = gate, a.gate_value = 1;
-        e = want_flat ? launch_ref_tracer(true, a, tiles * 4, depth, stats, s) : launch_fast(fa, waves, depth, stats, s);
+        e = want_flat ? launch_ref_tracer(true, a, tiles * 4, depth, stats, s) : launch_fast(trav(a), waves, depth, stats, s);
         if (e == hipSuccess) {
             RenderArgs r = a;
             r.tris = nullptr, r.gate_value = 0;
@@ -825,7 +834,7 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     else if (want_flat)
         e = launch_ref_tracer(true, a, tiles * 4, depth, stats, s);
     else if (want_wf)
-        e = g_experimental.load()->wavefront(fa, depth, s);
+        e = g_experimental.load()->wavefront(trav(a), depth, s);
     else if (lone) {
         // the lone-pixel kernel on a side stream forked from and joined back into the caller's
         LoneStreams* ls = lone_streams(s);
@@ -833,11 +842,11 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
         if (check(hipEventRecord(ls->fork, s), "hipEventRecord") || check(hipStreamWaitEvent(ls->side, ls->fork, 0), "hipStreamWaitEvent"))
             return 1;
         e = g_experimental.load()->lone(a, p->lone_slots, (int)p->lone_count, mir.treelets, ls->side);
-        if (e == hipSuccess) e = launch_fast(fa, waves, depth, stats, s);
+        if (e == hipSuccess) e = launch_fast(trav(a), waves, depth, stats, s);
         if (check(hipEventRecord(ls->join, ls->side), "hipEventRecord") || check(hipStreamWaitEvent(s, ls->join, 0), "hipStreamWaitEvent"))
             return 1;
     } else
-        e = launch_fast(fa, waves, depth, stats, s);
+        e = launch_fast(trav(a), waves, depth, stats, s);
     return check(e, "render_kernel launch");
 }
 

@@ -114,7 +114,7 @@ __device__ __forceinline__ void lone_leaf(const RenderArgs& a, const float4* tri
     if ((MODE & 4) && pf == 2u && a.tree && a.flat) {
         Trav T{f0, c0, 0};
         coop_tree<false>(tris, a.tree, a.ltris, a.flat, 1ull, po, R, h, T, scratch, a.tune, c);
-    } else if (pf == 1u && a.pairs) {
+    } else if ((pf & 1u) && a.pairs) {  // pf 3: a screen record precedes the pairs (mirror.h)
         coop_leaf(tris, a.pairs + 5 * (size_t)po, 1ull, f0, c0, R, h);
     } else {
         coop_leaf_scalar(tris, 1ull, f0, c0, R, h);

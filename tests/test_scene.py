@@ -131,3 +131,23 @@ def test_private_node_array(which):
     # the pairs are numbered in the order the DFS first reaches them (right-first pre-order)
     assert pairs_in_order == sorted(pairs_in_order)
     assert pairs_in_order[0] == 2 and pairs_in_order[-1] == prv.shape[0] - 2
+
+
+def test_big_leaf_screen_records():
+    """Big leaves whose core (all but the few big "outlier" triangles) has a normal cone narrow enough
+    for cluster_cull get a screen record (mirror.h pf = 3; rt_fast.h screen_leaf): the 4-bunny scene's
+    21-triangle leaf does; the bunny scene's 345-triangle floor leaf does not (its core's cone spans
+    ~90 degrees, so no ray could ever be culled and the screen would only cost)."""
+    rt = T.load_rt()
+    counts = {}
+    for which in ("bunny", "bunny4"):
+        s = rt.Scene()
+        s.setup(which)
+        s.build()
+        tris = s.mirror().view(np.uint32)
+        nodes = s.host_arrays()["nodes"].view(np.uint32).reshape(-1, 8)
+        big = nodes[(nodes[:, 7] > 8)]
+        pf = {int(n[7]): int(tris[n[6], 11]) for n in big}
+        counts[which] = pf
+    assert counts["bunny"] == {345: 1}
+    assert counts["bunny4"][21] == 3 and counts["bunny4"][12318] == 2 and counts["bunny4"][903] == 1

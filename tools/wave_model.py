@@ -168,7 +168,21 @@ def measure(args):
     np.savez_compressed(args.out, **out)
 
 
-def model(args):
+def fit_k0(args):
+    """The one free constant, k0, fitted to the measured shard times (least squares in log space over
+    the slowest rank of every N), beside the microbenchmark's 8.2 / 1.8."""
+    best = None
+    for k0 in np.arange(2.0, 8.01, 0.25):
+        a = argparse.Namespace(**vars(args))
+        a.k0 = float(k0)
+        s = model(a, quiet=True)
+        err = sum(np.log(v["model_ms"] / v["measured_ms"]) ** 2 for v in s.values())
+        if best is None or err < best[0]:
+            best = (err, float(k0))
+    return best[1]
+
+
+def model(args, quiet=False):
     d = np.load(args.model)
     keys = sorted({k.rsplit("_", 1)[0] for k in d.files})
     rows = []
@@ -195,9 +209,12 @@ def model(args):
                for n, v in sorted(by_n.items())}
     for v in summary.values():
         v["err"] = round(v["model_ms"] / v["measured_ms"] - 1, 3)
+    if quiet:
+        return summary
     for row in rows:
         print(json.dumps(row))
     print(json.dumps({"k0": args.k0, "slots": args.slots, "per_n_slowest_rank": summary}))
+    return summary
 
 
 def main():
@@ -213,10 +230,13 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "wave_model.npz"))
     ap.add_argument("--k0", type=float, default=8.2 / 1.8)
     ap.add_argument("--slots", type=int, default=7)
+    ap.add_argument("--fit", action="store_true", help="fit k0 to the measured shard times instead")
     args = ap.parse_args()
     if args.measure:
         measure(args)
     if args.model:
+        if args.fit:
+            args.k0 = fit_k0(args)
         model(args)
 
 
