@@ -1,6 +1,5 @@
 // rt_fast_prod.hip -- the production variants of the render kernel: MODE 17 (split small steps, pair
-// records; scenes without leaf trees) and 21 (the same with leaf trees), 49 / 53 the same for scenes with
-// big-leaf screen records (mirror.h pf = 3; rt_fast.h screen_leaf), each built for 5, 6 and 7 waves
+// records; scenes without leaf trees) and 21 (the same with leaf trees), each built for 5, 6 and 7 waves
 // per SIMD (rt_fast_body.h render_fast_kernel_w5 / _w6 / _w7; bench.py's occupancy probe picks one --
 // config 2 runs render_fast_kernel_w7<30, false, 17>).
 #include "rt_fast_body.h"
@@ -12,8 +11,6 @@ hipError_t dispatch(int mode, const RenderArgs& a, int waves, hipStream_t s) {
     switch (mode) {
         case 17: return launch_occ<STACK, false, 17>(a, waves, s);
         case 21: return launch_occ<STACK, false, 21>(a, waves, s);
-        case 49: return launch_occ<STACK, false, 49>(a, waves, s);  // 17 + big-leaf screens (MODE bit 5)
-        case 53: return launch_occ<STACK, false, 53>(a, waves, s);  // 21 + big-leaf screens
     }
     return hipErrorInvalidValue;
 }

@@ -1,6 +1,5 @@
 // rt_fast_timing.hip -- timing variants of the production kernel (MODE bit 3: phase clocks, per-pixel
-// work for rt_lane_plan, per-wave clock records): 25 (= 17 + timing), 29 (= 21 + timing), 57 / 61 (the
-// same with big-leaf screens), 9 (no split).
+// work for rt_lane_plan, per-wave clock records): 25 (= 17 + timing), 29 (= 21 + timing), 9 (no split).
 #include "rt_fast_body.h"
 
 namespace rtk {
@@ -10,8 +9,6 @@ hipError_t dispatch(int mode, const RenderArgs& a, int waves, hipStream_t s) {
     switch (mode) {
         case 25: return launch_occ<STACK, false, 25>(a, waves, s);
         case 29: return launch_occ<STACK, false, 29>(a, waves, s);
-        case 57: return launch_occ<STACK, false, 57>(a, waves, s);  // 25 + big-leaf screens
-        case 61: return launch_occ<STACK, false, 61>(a, waves, s);  // 29 + big-leaf screens
         case 9: return launch_occ<STACK, false, 9>(a, waves, s);
     }
     return hipErrorInvalidValue;

@@ -220,9 +220,10 @@ std::atomic<const ExperimentalKernels*> g_experimental{nullptr};
 
 // Whether a frame asks for a kernel of librt_hip_exp.so (rt_render.h): the non-split / big-leaf
 // A/B variants (RT_TUNE bits 12, 4-5), refill, the lone-pixel kernel, the wavefront tracer.
-bool needs_experimental(const rt_render_params* p, bool has_tree) {
+bool needs_experimental(const rt_render_params* p, bool has_tree, bool screens) {
     const bool stats = (p->flags & RT_RENDER_STATS) != 0;
     if ((p->flags & RT_RENDER_TRACER_WAVEFRONT) || p->refill_lanes || p->lone_count > 0) return true;
+    if (screens && (p->tune & 4096u) == 0 && (!stats || (p->tune & 256u))) return true;  // big-leaf screen variants
     if (stats || p->lane_cost) return false;  // statistics / timing families are in the product
     const uint32_t mode = (p->tune >> 4) & 3u;
     return (p->tune & 4096u) != 0 || (!has_tree && (mode == 2u || mode == 3u));
@@ -232,26 +233,33 @@ hipError_t launch_fast(const RenderArgs& args, int waves, int depth, bool stats,
     const int stack = (depth >= 0 && depth + 2 <= 30) ? 30 : (depth >= 0 && depth + 2 <= 40) ? 40 : 64;
     // statistics: the reference's work on scalar records (RT_TUNE bit 7: through the leaf trees);
     // RT_TUNE bit 8: a timing frame of the production kernel instead (phase clocks, no counts)
-    // MODE bit 5: big-leaf screens compiled in, for scenes whose mirror has screen records (mirror.h pf = 3)
-    const int sm = args.screens ? 32 : 0;
-    if (stats && (args.tune & 256u))
-        return launch_fast_timing(stack, args.tree ? 29 + sm : (args.tune & 4096u) ? 9 : 25 + sm, args, waves, s);
+    const ExperimentalKernels* x = g_experimental.load();  // rt_render refused these frames without it
+    // MODE bit 5 (librt_hip_exp.so): big-leaf screens, for scenes whose mirror has screen records
+    const bool scr = args.screens != 0 && (args.tune & 4096u) == 0;
+    if (stats && (args.tune & 256u)) {
+        if (scr) return x ? x->fast_screen(stack, args.tree ? 61 : 57, args, waves, s) : hipErrorNotSupported;
+        return launch_fast_timing(stack, args.tree ? 29 : (args.tune & 4096u) ? 9 : 25, args, waves, s);
+    }
     // per-pixel work (rt_render_params.lane_cost): the timing variant of the production kernel
-    if (!stats && args.lane_cost) return launch_fast_timing(stack, (args.tree ? 29 : 25) + sm, args, waves, s);
+    if (!stats && args.lane_cost) {
+        if (scr) return x ? x->fast_screen(stack, args.tree ? 61 : 57, args, waves, s) : hipErrorNotSupported;
+        return launch_fast_timing(stack, args.tree ? 29 : 25, args, waves, s);
+    }
     if (stats) return launch_fast_stats(stack, (args.tree && (args.tune & 128u)) ? 6 : 2, args, waves, s);
     // MODE bit 4: inner-node and small-leaf steps in separate iterations (rt_fast.h trace); RT_TUNE
     // bit 12 turns it off (A/B).  Big leaves: packed pairs in the shared-leaf loop, scalar records in
     // cooperative rounds (MODE 1, measured best); leaf trees compiled in only for scenes that have
     // them (MODE bit 2); A/B: RT_TUNE bits 4-5 = 2 scalar only, 3 pairs everywhere.
     const bool split = (args.tune & 4096u) == 0;
-    const ExperimentalKernels* x = g_experimental.load();  // rt_render refused these frames without it
     if (args.queue_head) return x ? x->fast_refill(stack, args.tree ? 85 : 81, args, waves, s) : hipErrorNotSupported;
+    if (scr && split && (args.tree || ((args.tune >> 4) & 3u) < 2u))
+        return x ? x->fast_screen(stack, args.tree ? 53 : 49, args, waves, s) : hipErrorNotSupported;
     if (args.tree) {
-        if (split) return launch_fast_prod(stack, 21 + sm, args, waves, s);
+        if (split) return launch_fast_prod(stack, 21, args, waves, s);
         return x ? x->fast_ab(stack, 5, args, waves, s) : hipErrorNotSupported;
     }
     const uint32_t mode = (args.tune >> 4) & 3u;
-    if (split && mode < 2) return launch_fast_prod(stack, 17 + sm, args, waves, s);
+    if (split && mode < 2) return launch_fast_prod(stack, 17, args, waves, s);
     if (!x) return hipErrorNotSupported;
     if (mode == 2) return x->fast_ab(stack, 2, args, waves, s);
     if (mode == 3) return x->fast_ab(stack, 0, args, waves, s);
@@ -787,7 +795,8 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     // its pixel state packs the sample count in 16 bits and the bounce in 8; a generation per segment
     if (want_wf && (p->spp > 65535 || p->bounces > 255 || (int64_t)p->spp * p->bounces > 65536))
         return set_error("rt_render: the wavefront tracer needs spp <= 65535, bounces <= 255, spp x bounces <= 65536");
-    if (!g_experimental.load() && needs_experimental(p, a.tree != nullptr))
+    a.screens = (mir.screens > 0 && (a.tune & (1u << 28)) == 0 && a.tris && !(p->flags & RT_RENDER_TRACER_FLAT)) ? 1 : 0;
+    if (!g_experimental.load() && needs_experimental(p, a.tree != nullptr, a.screens != 0))
         return set_error("rt_render: this frame asks for an experimental render path (wavefront tracer, refill, lone-pixel "
                          "kernel or an RT_TUNE A/B variant), which lives in librt_hip_exp.so -- load it first "
                          "(rt.load_experimental())");
@@ -809,7 +818,6 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
         if (check(hipMemsetAsync(a.queue_head, 0, sizeof(unsigned long long), s), "hipMemsetAsync") != 0) return 1;
     }
     a.scene_fast = scene_fast ? 1 : 0;
-    a.screens = (mir.screens > 0 && (a.tune & (1u << 28)) == 0) ? 1 : 0;  // RT_TUNE bit 28: no big-leaf screens
     // the traversal kernels read the mirror's private node array (mirror.h: 64-B aligned sibling
     // pairs in right-first pre-order; RT_TUNE bit 27: the reference's array instead, A/B); the
     // reference-layout tracers keep the reference's

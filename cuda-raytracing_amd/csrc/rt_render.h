@@ -22,6 +22,7 @@ hipError_t launch_ref_tracer(bool flat, const RenderArgs& a, int waves, int dept
 // accepts the flags / knobs that select them; without it those requests are refused).
 hipError_t launch_fast_ab(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);      // 1, 5, 2, 0
 hipError_t launch_fast_refill(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);  // 81, 85
+hipError_t launch_fast_screen(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);  // 49, 53, 57, 61
 // The lone-pixel kernel (rt_lone.hip): one wave per slot of `lone_slots`, through the treelets.
 hipError_t launch_lone(const RenderArgs& a, const int32_t* lone_slots, int lone_count, const void* treelets, hipStream_t s);
 // The wavefront tracer (rt_wavefront.hip): shade / trace launches per segment generation.
@@ -32,6 +33,7 @@ struct ExperimentalKernels {
     decltype(&launch_fast_refill) fast_refill;
     decltype(&launch_lone) lone;
     decltype(&launch_wavefront) wavefront;
+    decltype(&launch_fast_screen) fast_screen;
 };
 // rt_kernel.hip: the registered table (nullptr until librt_hip_exp.so is loaded).
 void register_experimental_kernels(const ExperimentalKernels* k);

@@ -456,7 +456,8 @@ typedef struct rt_build_options {
     float split_angle;        /* leaf trees: split by normals while the cone half-angle exceeds this, rad (0.03) */
     uint32_t bvh_small;       /* GPU BVH builder: nodes this small build their subtree in one thread, 2..64 (16) */
     int32_t host_bvh;         /* 1: rt_scene_upload always builds the BVH on the host (0: GPU from 65,536 faces) */
-    int32_t leaf_screens;     /* 1: big leaves whose core can be culled get a screen record (mirror.h pf = 3) (1) */
+    int32_t leaf_screens;     /* 1: big leaves whose core can be culled get a screen record (mirror.h pf = 3),
+                                 rendered by the screen variants of librt_hip_exp.so (A/B, measured slower) (0) */
 } rt_build_options;
 void rt_get_build_options(rt_build_options* out);
 int rt_set_build_options(const rt_build_options* options);  /* 0, or an error for out-of-range values */

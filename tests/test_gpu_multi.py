@@ -436,6 +436,31 @@ def test_lone_pixels_many_spheres(rt):
     assert np.array_equal(rng2.cpu().numpy(), rng_full)
 
 
+@pytest.mark.parametrize("wps", [5, 6, 7])
+def test_big_leaf_screens_equal_plain(rt, wps):
+    """The big-leaf screen variants (librt_hip_exp.so, rt_build_options.leaf_screens; rt_fast.h
+    screen_leaf: a lane whose ray provably misses a leaf's core tests only its outliers) render the
+    4-bunny frame and RNG states bit for bit as the production kernel without screens, at every
+    occupancy (a per-lane bool for the screened state once mis-rendered at 6 waves per SIMD)."""
+    w, h, spp, bounces = 256, 144, 4, 6
+    res = {}
+    rt.set_build_options(leaf_screens=1)
+    try:
+        for tune in (0, 1 << 28):  # bit 28: screens off
+            s = scene(rt, w, h, "bunny4")
+            rng = rt.alloc_rng(w * h)
+            rt.init_rng_states(rng, w, h, T.SEED)
+            s.upload(rng.data_ptr())
+            a, b = rt.alloc_surface(w, h), rt.alloc_surface(w, h)
+            rt.render(s, a, b, w, h, spp, bounces, 0, waves_per_simd=wps, tune=tune)
+            torch.cuda.synchronize()
+            res[tune] = (rt.surface_view(a, w).cpu().numpy().copy(), rng.cpu().numpy().copy())
+    finally:
+        rt.set_build_options()
+    assert np.array_equal(res[0][0].view(np.uint32), res[1 << 28][0].view(np.uint32))
+    assert np.array_equal(res[0][1], res[1 << 28][1])
+
+
 def test_lone_and_lane_overlap_is_caught(rt):
     """A slot in both lone_slots and lane_slots would be rendered twice at once (undefined results,
     rt_abi.h); RT_RENDER_VALIDATE finds it on the device before anything is launched."""

@@ -134,20 +134,31 @@ def test_private_node_array(which):
 
 
 def test_big_leaf_screen_records():
-    """Big leaves whose core (all but the few big "outlier" triangles) has a normal cone narrow enough
-    for cluster_cull get a screen record (mirror.h pf = 3; rt_fast.h screen_leaf): the 4-bunny scene's
-    21-triangle leaf does; the bunny scene's 345-triangle floor leaf does not (its core's cone spans
-    ~90 degrees, so no ray could ever be culled and the screen would only cost)."""
+    """With rt_build_options.leaf_screens, big leaves whose core (all but the few big "outlier"
+    triangles) has a normal cone narrow enough for cluster_cull get a screen record (mirror.h pf = 3;
+    rt_fast.h screen_leaf): the 4-bunny scene's 21-triangle leaf does; the bunny scene's 345-triangle
+    floor leaf does not (its core's cone spans ~90 degrees, so no ray could ever be culled)."""
     rt = T.load_rt()
     counts = {}
-    for which in ("bunny", "bunny4"):
+    rt.set_build_options(leaf_screens=1)  # an opt-in A/B (measured slower on config 4)
+    try:
+        for which in ("bunny", "bunny4"):
+            counts[which] = _big_leaf_flags(rt, which)
+        assert _big_leaf_flags(rt, "bunny4")[21] == 3
+    finally:
+        rt.set_build_options()
+    assert _big_leaf_flags(rt, "bunny4")[21] == 1, "off by default"
+    assert counts["bunny"] == {345: 1}
+    assert counts["bunny4"][21] == 3 and counts["bunny4"][12318] == 2 and counts["bunny4"][903] == 1
+
+
+def _big_leaf_flags(rt, which):
+    """{leaf size: pf} of a scene's big leaves (mirror.h lead records)."""
+    if True:
         s = rt.Scene()
         s.setup(which)
         s.build()
         tris = s.mirror().view(np.uint32)
         nodes = s.host_arrays()["nodes"].view(np.uint32).reshape(-1, 8)
         big = nodes[(nodes[:, 7] > 8)]
-        pf = {int(n[7]): int(tris[n[6], 11]) for n in big}
-        counts[which] = pf
-    assert counts["bunny"] == {345: 1}
-    assert counts["bunny4"][21] == 3 and counts["bunny4"][12318] == 2 and counts["bunny4"][903] == 1
+        return {int(n[7]): int(tris[n[6], 11]) for n in big}

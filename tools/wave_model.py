@@ -38,6 +38,24 @@ SIMDS = 1024
 CLOCK_HZ = 100e6  # wave_clock ticks (s_memrealtime)
 
 
+DISPATCH = "rr"  # initial placement: "rr" wave g -> SIMD g mod 1024; "fill" 7 per SIMD in order; "xcd" see below
+
+
+def initial_simd(i):
+    """SIMD of the i-th dispatched wave (i < slots x SIMDs)."""
+    if DISPATCH == "fill":
+        return i // SLOTS
+    if DISPATCH == "xcd":  # round-robin over the 8 XCDs, then over each XCD's 32 CUs, then a CU's 4 SIMDs
+        x, j = i % 8, i // 8
+        cu, k = j % 32, j // 32
+        return ((x * 32 + cu) * 4 + k % 4) % SIMDS
+    return i % SIMDS
+
+
+SLOTS = 7
+C0 = 1e9  # CU-level saturation (waves per CU at which the CU's shared memory path saturates); off by default
+
+
 def simulate(alone_ms, k0, slots, order=None):
     """Processor-sharing simulation of one launch: `alone_ms[g]` = wave g's chain alone (ms), waves
     dispatched in order g = 0, 1, ... to SIMD g mod SIMDS while slots last, then into freed slots.
@@ -53,8 +71,10 @@ def simulate(alone_ms, k0, slots, order=None):
     heap = []  # (predicted finish, simd, version)
     version = np.zeros(SIMDS, dtype=np.int64)
 
+    cu_n = np.zeros(SIMDS // 4, dtype=np.int64)  # waves resident per CU (4 SIMDs)
+
     def rate(s):
-        return 1.0 / max(1.0, len(resident[s]) / k0)
+        return 1.0 / max(1.0, len(resident[s]) / k0, cu_n[s // 4] / C0)
 
     def advance(s, t):
         r = rate(s) if resident[s] else 0.0
@@ -68,34 +88,43 @@ def simulate(alone_ms, k0, slots, order=None):
             w = min(resident[s], key=lambda x: rem[x])
             heapq.heappush(heap, (t_last[s] + max(rem[w], 0.0) / rate(s), s, version[s]))
 
-    # initial dispatch: round-robin over the SIMDs, `slots` deep
-    for depth in range(slots):
-        for s in range(SIMDS):
-            if nxt >= n:
-                break
-            g = order[nxt]
-            resident[s].append(g)
-            simd_of[g] = s
-            nxt += 1
+    # initial dispatch (DISPATCH), `slots` deep
+    global SLOTS
+    SLOTS = slots
+    while nxt < n and nxt < slots * SIMDS:
+        s = initial_simd(nxt)
+        if len(resident[s]) >= slots:  # placement collision: the next SIMD with a free slot
+            s = next(t % SIMDS for t in range(s, s + SIMDS) if len(resident[t % SIMDS]) < slots)
+        g = order[nxt]
+        resident[s].append(g)
+        simd_of[g] = s
+        nxt += 1
+    for s in range(SIMDS):
+        cu_n[s // 4] += len(resident[s])
     for s in range(SIMDS):
         schedule(s)
     while heap:
         t, s, v = heapq.heappop(heap)
         if v != version[s]:
             continue
-        advance(s, t)
+        cu = s // 4
+        for q in range(4 * cu, 4 * cu + 4):  # the CU's SIMDs share the CU term: bring them all to t
+            advance(q, t)
         done = [w for w in resident[s] if rem[w] <= 1e-12]
         if not done:  # numerical slack
             done = [min(resident[s], key=lambda x: rem[x])]
         for w in done:
             resident[s].remove(w)
             finish[w] = t
+            cu_n[cu] -= 1
             if nxt < n:  # the freed slot takes the next wave in dispatch order
                 g = order[nxt]
                 resident[s].append(g)
                 simd_of[g] = s
+                cu_n[cu] += 1
                 nxt += 1
-        schedule(s)
+        for q in range(4 * cu, 4 * cu + 4):
+            schedule(q)
     return finish, simd_of
 
 
@@ -157,10 +186,26 @@ def measure(args):
             shard_ms = float(np.mean([frames(clock=False, waves_per_simd=args.wps)[0] for _ in range(2)]))
             full_ms, t_full = frames(waves_per_simd=args.wps)
             alone_shard_ms, t_alone = frames(waves_per_simd=1)
+            # one timing frame (RT_TUNE 256 + 2048) at the same occupancy: every wave's start and end on
+            # the 100 MHz device clock, indexed by hardware workgroup (dispatch order)
+            st = torch.zeros(24 + 8 * waves, dtype=torch.int64, device="cuda")
+            rt.render(scene, None, None, W, H, SPP, BOUNCES, 0, 0, 1, out_shard=buf, tile_list=mine, lane_slots=lm,
+                      stats=st, tune=256 | 2048, waves_per_simd=args.wps)
+            torch.cuda.synchronize()
+            rng.copy_(saved)
+            rec = st[24:].view(-1, 8).cpu().numpy()
+            t0 = rec[:, 0].min()
+            out[f"n{n}_r{r}_start"] = (rec[:, 0] - t0) / CLOCK_HZ * 1e3
+            out[f"n{n}_r{r}_end"] = (rec[:, 1] - t0) / CLOCK_HZ * 1e3
             pix = (lm.view(-1, 64) >= 0).sum(1).cpu().numpy() if lm is not None else np.full(waves, 64)
             key = f"n{n}_r{r}"
             out[key + "_full"], out[key + "_alone"], out[key + "_pixels"] = t_full, t_alone, pix
             out[key + "_meta"] = np.array([shard_ms, full_ms, alone_shard_ms, n, r, waves])
+            se = out[f"n{n}_r{r}_start"], ee = out[f"n{n}_r{r}_end"]
+            print(json.dumps({"n": n, "rank": r, "timing_frame": {"start_ms_p50_p99_max": [round(float(np.percentile(se, q)), 4) for q in (50, 99, 100)],
+                                                                 "last_end_ms": round(float(ee.max()), 3),
+                                                                 "longest_ms": round(float((ee - se).max()), 3),
+                                                                 "end_of_longest_ms": round(float(ee[np.argmax(ee - se)]), 3)}}), flush=True)
             print(json.dumps({"n": n, "rank": r, "waves": int(waves), "shard_ms": round(shard_ms, 3),
                               "clocked_frame_ms": round(full_ms, 3), "capped1_frame_ms": round(alone_shard_ms, 3),
                               "wave_full_ms_max": round(float(t_full.max()), 3), "wave_alone_ms_max": round(float(t_alone.max()), 3),
@@ -184,7 +229,7 @@ def fit_k0(args):
 
 def model(args, quiet=False):
     d = np.load(args.model)
-    keys = sorted({k.rsplit("_", 1)[0] for k in d.files})
+    keys = sorted({k.rsplit("_", 1)[0] for k in d.files if k.endswith("_meta")})
     rows = []
     for key in keys:
         meta = d[key + "_meta"]
@@ -231,7 +276,12 @@ def main():
     ap.add_argument("--k0", type=float, default=8.2 / 1.8)
     ap.add_argument("--slots", type=int, default=7)
     ap.add_argument("--fit", action="store_true", help="fit k0 to the measured shard times instead")
+    ap.add_argument("--dispatch", default="rr", choices=["rr", "fill", "xcd"], help="initial wave placement")
+    ap.add_argument("--c0", type=float, default=0.0, help="CU-level saturation in waves per CU (0 = off)")
     args = ap.parse_args()
+    global DISPATCH, C0
+    DISPATCH = args.dispatch
+    C0 = args.c0 if args.c0 > 0 else 1e9
     if args.measure:
         measure(args)
     if args.model:
