@@ -201,7 +201,7 @@ def measure(args):
             key = f"n{n}_r{r}"
             out[key + "_full"], out[key + "_alone"], out[key + "_pixels"] = t_full, t_alone, pix
             out[key + "_meta"] = np.array([shard_ms, full_ms, alone_shard_ms, n, r, waves])
-            se = out[f"n{n}_r{r}_start"], ee = out[f"n{n}_r{r}_end"]
+            se, ee = out[f"n{n}_r{r}_start"], out[f"n{n}_r{r}_end"]
             print(json.dumps({"n": n, "rank": r, "timing_frame": {"start_ms_p50_p99_max": [round(float(np.percentile(se, q)), 4) for q in (50, 99, 100)],
                                                                  "last_end_ms": round(float(ee.max()), 3),
                                                                  "longest_ms": round(float((ee - se).max()), 3),
