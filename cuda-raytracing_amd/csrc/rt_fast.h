@@ -1192,6 +1192,16 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
 #ifdef RT_LANE_HIST  // diagnostic build: wave cycles of small-step iterations by active-lane count
                 const unsigned long long th0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
 #endif
+#ifdef RT_COMBINE_T
+                // few lanes of both kinds: one iteration serves both (their loads overlap; the split
+                // exists to gather lanes per kind, which matters little when both groups are small)
+                if (!scr_on && mI && mL && nI + nL <= (uint32_t)RT_COMBINE_T) {
+                    if (inner || leafs) {
+                        active = small_step<STATS>(nodes4, tris, spairs, stk, R, h, T, c);
+                        if (TIMING) c.lane_work++;
+                    }
+                } else
+#endif
                 if (!mI || nL * 4u >= nI * (q + 1u)) {
                     if (leafs) {
                         active = small_step<STATS, scr_on>(nodes4, tris, spairs, stk, R, h, T, c, pairs);

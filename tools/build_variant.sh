@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build a librt_hip.so variant with extra compile definitions for the production family only:
 #   bash tools/build_variant.sh NAME "-DFOO=1"  ->  cuda-raytracing_amd/variants/v_NAME.so
-# (the other objects are the current build's; run tools/gpu_variants.sh VARS="NAME new" to A/B)
+# (the other product objects are the current build's; A/B with VARS="current NAME" bash tools/gpu_ab.sh)
 set -e
 cd "$(dirname "$0")/.."
 name="$1"; shift
@@ -12,7 +12,11 @@ mkdir -p "$V" /tmp/rtvar
   -I include -I cuda-raytracing_amd/csrc -c cuda-raytracing_amd/csrc/rt_fast_prod.hip -o /tmp/rtvar/prod_$name.o
 objs=""
 for o in $B/*.o; do
-  case "$o" in *rt_fast_prod.hip.o) objs="$objs /tmp/rtvar/prod_$name.o";; *) objs="$objs $o";; esac
+  case "$o" in
+    *rt_fast_prod.hip.o) objs="$objs /tmp/rtvar/prod_$name.o";;
+    *rt_fast_ab*|*rt_fast_refill*|*rt_fast_screen*|*rt_lone*|*rt_wavefront*|*rt_exp*) ;;  # the plugin's (librt_hip_exp.so)
+    *) objs="$objs $o";;
+  esac
 done
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $objs -L/opt/rocm/lib -lrccl -o "$V/v_$name.so"
 echo "built $V/v_$name.so"

@@ -167,7 +167,10 @@ def measure(args):
             waves = lm.numel() // 64 if lm is not None else mine.numel() * 4
 
             def frames(clock=True, **kw):
-                ms, acc = [], np.zeros(waves, dtype=np.int64)
+                """three consecutive frames of the RNG chain from the saved states: per-frame event
+                time and per-frame wave clocks (frames differ -- each its own random paths -- and the
+                same three frames are replayed for every occupancy)"""
+                ms, per = [], []
                 clk = torch.zeros(waves, dtype=torch.int64, device="cuda")
                 if clock:
                     kw["wave_clock"] = clk
@@ -179,13 +182,18 @@ def measure(args):
                     e1.record()
                     torch.cuda.synchronize()
                     ms.append(e0.elapsed_time(e1))
-                    acc += bench.sanitize_wave_clocks(clk.cpu().numpy())[0].astype(np.int64)
+                    per.append(bench.sanitize_wave_clocks(clk.cpu().numpy())[0] / CLOCK_HZ * 1e3)
                 rng.copy_(saved)
-                return float(np.mean(ms)), acc / 3.0 / CLOCK_HZ * 1e3
+                return np.array(ms), np.array(per)
 
-            shard_ms = float(np.mean([frames(clock=False, waves_per_simd=args.wps)[0] for _ in range(2)]))
-            full_ms, t_full = frames(waves_per_simd=args.wps)
-            alone_shard_ms, t_alone = frames(waves_per_simd=1)
+            shard_ms = float(np.mean([frames(clock=False, waves_per_simd=args.wps)[0].mean() for _ in range(2)]))
+            full_frames_ms, full_per = frames(waves_per_simd=args.wps)
+            alone_frames_ms, alone_per = frames(waves_per_simd=1)
+            full_ms, alone_shard_ms = float(full_frames_ms.mean()), float(alone_frames_ms.mean())
+            t_full, t_alone = full_per.mean(0), alone_per.mean(0)
+            out[f"n{n}_r{r}_frames_ms"] = full_frames_ms
+            out[f"n{n}_r{r}_alone_per_frame"] = alone_per.astype(np.float32)
+            out[f"n{n}_r{r}_full_per_frame"] = full_per.astype(np.float32)
             # one timing frame (RT_TUNE 256 + 2048) at the same occupancy: every wave's start and end on
             # the 100 MHz device clock, indexed by hardware workgroup (dispatch order)
             st = torch.zeros(24 + 8 * waves, dtype=torch.int64, device="cuda")
@@ -236,8 +244,18 @@ def model(args, quiet=False):
         shard_ms, n, r, waves = float(meta[0]), int(meta[3]), int(meta[4]), int(meta[5])
         alone, full, pix = d[key + "_alone"], d[key + "_full"], d[key + "_pixels"]
         lb = xcd_order(waves)  # hardware dispatch order g -> logical wave lb
-        fin, simd = simulate(alone, args.k0, args.slots, order=lb)
-        pred = float(fin.max())
+        if key + "_alone_per_frame" in d.files:
+            # frame by frame: each frame's own waves (the longest wave differs from frame to frame, and
+            # a strong-scaled frame ends with its longest), against that frame's measured time
+            per = d[key + "_alone_per_frame"].astype(np.float64)
+            preds = [float(simulate(a, args.k0, args.slots, order=lb)[0].max()) for a in per]
+            shard_ms = float(d[key + "_frames_ms"].mean())
+            fin, simd = simulate(per[int(np.argmax(preds))], args.k0, args.slots, order=lb)
+            alone = per[int(np.argmax(preds))]
+            pred = float(np.mean(preds))
+        else:
+            fin, simd = simulate(alone, args.k0, args.slots, order=lb)
+            pred = float(fin.max())
         crit = int(simd[int(np.argmax(fin))])
         on = np.flatnonzero(simd == crit)
         rows.append({"n": n, "rank": r, "waves": waves, "measured_ms": round(shard_ms, 3), "model_ms": round(pred, 3),
@@ -262,6 +280,32 @@ def model(args, quiet=False):
     return summary
 
 
+def whatif(args):
+    """The model's answer to the two levers, on the slowest rank of every N: every chain shorter by 10 /
+    20 / 30 % (a faster kernel), or the waves above a threshold split in two halves of 0.79x their
+    alone time each (the measured cost of halving a wave's pixels), dispatched longest first."""
+    d = np.load(args.model)
+    keys = sorted({k.rsplit("_", 1)[0] for k in d.files if k.endswith("_meta")})
+    worst = {}
+    for key in keys:
+        meta = d[key + "_meta"]
+        n = int(meta[3])
+        if n not in worst or meta[0] > d[worst[n] + "_meta"][0]:
+            worst[n] = key
+    for n, key in sorted(worst.items()):
+        a = d[key + "_alone"]
+        out = {"n": n, "rank": int(d[key + "_meta"][4]), "measured_ms": round(float(d[key + "_meta"][0]), 3),
+               "model_ms": round(float(simulate(a, args.k0, args.slots, order=xcd_order(len(a)))[0].max()), 3)}
+        for f in (0.9, 0.8, 0.7):
+            out[f"chain_x{f}"] = round(float(simulate(a * f, args.k0, args.slots, order=xcd_order(len(a)))[0].max()), 3)
+        for thr in (3.0, 2.5, 2.0):
+            big = a > thr
+            b = np.concatenate([a[~big], np.repeat(a[big] * 0.79, 2)])
+            b = b[np.argsort(-b)]
+            out[f"split_above_{thr}ms"] = [round(float(simulate(b, args.k0, args.slots)[0].max()), 3), int(b.size)]
+        print(json.dumps(out))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--measure", action="store_true")
@@ -278,6 +322,7 @@ def main():
     ap.add_argument("--fit", action="store_true", help="fit k0 to the measured shard times instead")
     ap.add_argument("--dispatch", default="rr", choices=["rr", "fill", "xcd"], help="initial wave placement")
     ap.add_argument("--c0", type=float, default=0.0, help="CU-level saturation in waves per CU (0 = off)")
+    ap.add_argument("--whatif", action="store_true", help="also price the two levers (shorter chains, split waves)")
     args = ap.parse_args()
     global DISPATCH, C0
     DISPATCH = args.dispatch
@@ -288,6 +333,8 @@ def main():
         if args.fit:
             args.k0 = fit_k0(args)
         model(args)
+        if args.whatif:
+            whatif(args)
 
 
 if __name__ == "__main__":
