@@ -541,7 +541,7 @@ def run(args):
     wd.phase = "scene set-up and plans"
     assert world == args.gpus or args.pmc_child, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     rt = G.load_package()
-    if args.tracer != "fast" or args.refill or (args.tune & 0x101030):  # bit 20: treelet lone walk
+    if args.tracer != "fast" or args.refill or (args.tune & 0x1030):
         rt.load_experimental()  # A/B render paths (librt_hip_exp.so); the production path never needs it
     if args.build_options:  # exact-preserving mirror / BVH builder knobs (rt_set_build_options)
         rt.set_build_options(**{k: float(v) if k == "split_angle" else int(v)

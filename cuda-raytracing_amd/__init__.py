@@ -155,7 +155,6 @@ SIGNATURES = {
     "rt_scene_mirror_info": (_I, [_P, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
     "rt_scene_mirror_copy": (_I, [_P, _P, _P, _P]),
     "rt_scene_mirror_nodes": (_I, [_P, _P, ctypes.POINTER(_SZ)]),
-    "rt_scene_mirror_treelets": (_I, [_P, _P, ctypes.POINTER(_SZ), _P, ctypes.POINTER(_SZ)]),
     "rt_cluster_cull_host": (_I, [_P, _P, ctypes.c_float, _P]),
     "rt_xorwow_jump_matrix": (_I, [_I, ctypes.POINTER(ctypes.c_uint32)]),
     "rt_xorwow_init_host": (None, [_U32, _U64, _P]),
@@ -321,19 +320,6 @@ class Scene:
         out = np.zeros((n.value, 8), dtype=np.float32)
         _check(lib().rt_scene_mirror_nodes(self.handle, out.ctypes.data, ctypes.byref(n)), "rt_scene_mirror_nodes")
         return out
-
-    def mirror_treelets(self):
-        """The treelets (mirror.h) as (T, 64, 12) float32 and the inner nodes' treelet locations
-        (mirror.h tlloc) as uint32, indexed by private first_index."""
-        import numpy as np
-        nt, nl = ctypes.c_size_t(), ctypes.c_size_t()
-        _check(lib().rt_scene_mirror_treelets(self.handle, None, ctypes.byref(nt), None, ctypes.byref(nl)),
-               "rt_scene_mirror_treelets")
-        tl = np.zeros((nt.value, 64, 12), dtype=np.float32)
-        loc = np.zeros(nl.value, dtype=np.uint32)
-        _check(lib().rt_scene_mirror_treelets(self.handle, tl.ctypes.data, ctypes.byref(nt), loc.ctypes.data,
-                                              ctypes.byref(nl)), "rt_scene_mirror_treelets")
-        return tl, loc
 
     def host_arrays(self):
         """numpy copies of the host arrays: nodes (N,8) f32/u32 view, face indices, vertices, faces."""

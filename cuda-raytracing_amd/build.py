@@ -38,8 +38,8 @@ HIP_SOURCES = ["rt_fast_prod.hip", "rt_fast_timing.hip", "rt_fast_stats.hip", "r
 # librt_hip_exp.so: the exact alternatives kept for A/B measurement and their parity tests (A/B kernel
 # variants, refill, the lone-pixel kernel, the wavefront tracer); loading it registers them with
 # librt_hip.so (rt_render.h ExperimentalKernels, rt.load_experimental())
-EXP_SOURCES = ["rt_fast_ab.hip", "rt_fast_ab2.hip", "rt_fast_refill.hip", "rt_fast_screen.hip", "rt_fast_tl.hip", "rt_lone.hip",
-               "rt_wavefront.hip", "rt_exp.hip"]
+EXP_SOURCES = ["rt_fast_ab.hip", "rt_fast_ab2.hip", "rt_fast_refill.hip", "rt_fast_screen.hip", "rt_lone.hip", "rt_wavefront.hip",
+               "rt_exp.hip"]
 EXP_LIB = os.path.join(PKG, "librt_hip_exp.so")
 
 

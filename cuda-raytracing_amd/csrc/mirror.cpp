@@ -136,7 +136,7 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
     // every root's K3.x: the leaf-tree triangle count, the stride of their field-major device copy
     const uint32_t nl = (uint32_t)(out->ltris.size() / 12);
     for (uint32_t r : roots) std::memcpy(&out->tree[(size_t)r * 16 + 12], &nl, 4);
-    rt_build_treelets(nodes, node_count, out->treelets, &out->tlloc);
+    rt_build_treelets(nodes, node_count, out->treelets);
     rt_build_private_nodes(nodes, node_count, out->nodes);
 }
 
@@ -149,10 +149,10 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
 // 3 + 2p; an inner node's first_index is its left child's slot, a leaf's is unchanged (the
 // triangle range the tris / pair records are indexed by).  Same boxes, same visit order: the
 // traversal's decisions are the reference's.
-std::vector<uint32_t> rt_private_slots(const GPUBVHNode* nodes, size_t node_count, size_t* slots) {
+void rt_build_private_nodes(const GPUBVHNode* nodes, size_t node_count, std::vector<float>& out) {
+    out.clear();
+    if (node_count == 0) return;
     std::vector<uint32_t> slot(node_count, ~0u);  // private slot of every reachable node
-    *slots = 0;
-    if (node_count == 0) return slot;
     slot[0] = 0;
     uint32_t pairs = 0;
     std::vector<uint32_t> st{0u};
@@ -167,16 +167,7 @@ std::vector<uint32_t> rt_private_slots(const GPUBVHNode* nodes, size_t node_coun
         st.push_back(l);
         st.push_back(r);  // popped first
     }
-    *slots = 2 + 2 * (size_t)pairs;
-    return slot;
-}
-
-void rt_build_private_nodes(const GPUBVHNode* nodes, size_t node_count, std::vector<float>& out) {
-    out.clear();
-    if (node_count == 0) return;
-    size_t n = 0;
-    const std::vector<uint32_t> slot = rt_private_slots(nodes, node_count, &n);
-    out.assign(n * 8, 0.0f);
+    out.assign((size_t)(2 + 2 * pairs) * 8, 0.0f);
     for (size_t v = 0; v < node_count; v++) {
         if (slot[v] == ~0u) continue;
         GPUBVHNode nd = nodes[v];
@@ -199,19 +190,9 @@ std::vector<float> rt_ltris_device_layout(const std::vector<float>& ltris) {
 // its own treelet.  Within a treelet the nodes are stored in right-first preorder (first + 1
 // before first, the reference's pop order), so a slot's subtree is the run of slots after it.
 // ---------------------------------------------------------------------------------------
-void rt_build_treelets(const GPUBVHNode* nodes, size_t node_count, std::vector<float>& out, std::vector<float>* tlloc) {
+void rt_build_treelets(const GPUBVHNode* nodes, size_t node_count, std::vector<float>& out) {
     out.clear();
-    if (tlloc) tlloc->clear();
     if (node_count == 0 || nodes[0].prim_count > 0) return;  // a leaf root: nothing to walk
-    size_t nslots = 0;
-    std::vector<uint32_t> pslot;
-    if (tlloc) {
-        pslot = rt_private_slots(nodes, node_count, &nslots);
-        const uint32_t none = ~0u;
-        float fnone;
-        std::memcpy(&fnone, &none, 4);
-        tlloc->assign(nslots, fnone);
-    }
     constexpr uint32_t EMPTY = 0xffffffffu;
     const float inf = INFINITY;
     std::vector<uint32_t> roots{0u};
@@ -259,12 +240,6 @@ void rt_build_treelets(const GPUBVHNode* nodes, size_t node_count, std::vector<f
                 X = (uint32_t)roots.size();
                 roots.push_back(slots[p].node);
                 frontier = 1u;
-            } else if (cnt == 0 && tlloc) {
-                // taken with its children: X = the pushed left child's private slot, and the node's
-                // own location under its children's private slot (mirror.h tlloc)
-                X = pslot[nd.first_index];
-                const uint32_t loc = (uint32_t)(k << 6) | p;
-                std::memcpy(&(*tlloc)[X], &loc, 4);
             }
             std::memcpy(&o[6], &X, 4);
             std::memcpy(&o[7], &cnt, 4);
@@ -301,16 +276,16 @@ int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owne
     const std::vector<float> lt = rt_ltris_device_layout(m.ltris);
     // the parts in one block, each starting on a 256-B boundary (pairs of nodes and records on
     // cache-line boundaries: mirror.h)
-    const std::vector<float>* parts[9] = {&m.nodes, &m.tris, &m.pairs, &m.tree, &lt, &m.spairs, &m.flat, &m.treelets, &m.tlloc};
-    size_t off[9], total = 0;
-    for (int i = 0; i < 9; i++) {
+    const std::vector<float>* parts[8] = {&m.nodes, &m.tris, &m.pairs, &m.tree, &lt, &m.spairs, &m.flat, &m.treelets};
+    size_t off[8], total = 0;
+    for (int i = 0; i < 8; i++) {
         off[i] = total;
         total += (parts[i]->size() * 4 + 255) & ~(size_t)255;
     }
     void* block = nullptr;
     if (rt_malloc(&block, total + 256) != 0) return -1;
     char* b = static_cast<char*>(block);
-    for (int i = 0; i < 9; i++)
+    for (int i = 0; i < 8; i++)
         if (!parts[i]->empty() && rt_memcpy_h2d(b + off[i], parts[i]->data(), parts[i]->size() * 4) != 0) {
             rt_free(block);
             return -1;
@@ -325,7 +300,6 @@ int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owne
     e.dev.spairs = at(5);
     e.dev.flat = at(6);
     e.dev.treelets = at(7);
-    e.dev.tlloc = at(8);
     e.dev.depth = m.depth;
     e.dev.fast = m.fast;
     e.dev.screens = m.screens;

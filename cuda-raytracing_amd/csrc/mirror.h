@@ -30,11 +30,6 @@
 //           mask lo, hi, subtree size in slots, frontier) -- X = the leaf's first triangle, or for
 //           a frontier (an inner node whose children were not taken) the treelet rooted at it,
 //           which holds the same node again in its slot 0; unused slots have count = ~0u;
-//           an inner node taken with its children has X = its private first_index (the left
-//           child's slot in `nodes`, below), the entry the reference's DFS pushes for it;
-//  * tlloc  per private node slot s that is an inner node's first_index: (treelet << 6) | slot of
-//           that inner node in the treelet that holds its children -- where a lone lane at the node
-//           continues its walk through the treelets (rt_fast.h lone_treelet); ~0u elsewhere;
 //  * nodes  the traversal's private copy of the BVH nodes (rt_fast.h reads only this one): the
 //           reference's nodes renumbered so that every sibling pair starts on a 64-B boundary (the
 //           reference's 32-B root shifts half its pairs across two cache lines) and pairs follow the
@@ -64,7 +59,6 @@ struct MirrorHost {
     std::vector<float> ltris;     // 12 floats per leaf-tree triangle record
     std::vector<float> flat;      // 16 floats per record: leaf trees' flat cluster / cut lists
     std::vector<float> treelets;  // 64 slots x 12 floats per treelet (rt_lone.hip)
-    std::vector<float> tlloc;     // uint32 per private node slot: treelet location (rt_fast.h lone_treelet)
     int depth = 0;                // deepest leaf (root = 0) reachable from node 0
     bool fast = true;             // node bounds inside the filtered-slab range (rt_fast.h)
     int screens = 0;              // big leaves with a screen record (pf = 3)
@@ -83,14 +77,8 @@ std::vector<float> rt_ltris_device_layout(const std::vector<float>& ltris);
 // The private node array alone (also called by rt_build_mirror).
 void rt_build_private_nodes(const GPUBVHNode* nodes, size_t node_count, std::vector<float>& out);
 
-// The private slot of every node reachable from the root (~0u for the others); `slots` = the
-// private array's length in nodes.
-std::vector<uint32_t> rt_private_slots(const GPUBVHNode* nodes, size_t node_count, size_t* slots);
-
-// The treelets alone (also called by rt_build_mirror); with `tlloc`, also the treelet location of
-// every inner node (mirror.h tlloc), and inner nodes' X = their private first_index.
-void rt_build_treelets(const GPUBVHNode* nodes, size_t node_count, std::vector<float>& out,
-                       std::vector<float>* tlloc = nullptr);
+// The treelets alone (also called by rt_build_mirror).
+void rt_build_treelets(const GPUBVHNode* nodes, size_t node_count, std::vector<float>& out);
 
 // Registry: device copies of a mirror, keyed by the GPUScene's BVH node pointer and valid
 // while the scene's face_indices / faces / vertices pointers are the ones it was built from.
@@ -103,7 +91,6 @@ struct MirrorDevice {
     const void* ltris = nullptr;
     const void* flat = nullptr;
     const void* treelets = nullptr;
-    const void* tlloc = nullptr;
     int depth = -1;
     bool fast = false;
     int screens = 0;

@@ -61,14 +61,12 @@ struct RenderArgs {
     const float4* ltris;  // their triangle records
     const float4* spairs; // small leaves' triangles in packed pairs, pair (i, i+1) at record i, or null
     const float4* flat;   // leaf trees' flat cluster / cut lists (leaftree.h) or null
-    const float4* treelets;  // MODE bit 7 (lone rays through the treelets): the mirror's treelets, or null
-    const uint32_t* tlloc;   // ... and the treelet location of every inner node (mirror.h tlloc)
     // Diagnostic A/B knobs (rt_render_params.tune; 0 = the production path, every setting exact):
     //   bit 0 no cooperative leaf rounds, 1 no pair records, 2 no leaf trees, 3 no small-leaf pairs,
     //   4-5 big-leaf mode (launch_fast_t), 7 statistics through the leaf trees, 8 timing frame (phase
     //   clocks), 9-10 occupancy override (1 compiler's choice, 2 = 6, 3 = 7 waves per SIMD),
     //   11 per-wave clock records, 12 no split small steps, 13-15 split threshold, 16-19 XCD run
-    //   length (xcd_block), 20 lone rays through the treelets (MODE bit 7), 26 no lone-ray traversal, 27 the reference's node array instead of the
+    //   length (xcd_block), 26 no lone-ray traversal, 27 the reference's node array instead of the
     //   mirror's private one (rt_kernel.hip), 28 no big-leaf screens, 30 per-lane leaf-tree walk,
     //   31 subtree order.
     uint32_t tune;

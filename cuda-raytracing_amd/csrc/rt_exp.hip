@@ -6,8 +6,7 @@
 
 namespace rtk {
 namespace {
-const ExperimentalKernels kTable{launch_fast_ab, launch_fast_refill, launch_lone, launch_wavefront, launch_fast_screen,
-                                 launch_fast_tl};
+const ExperimentalKernels kTable{launch_fast_ab, launch_fast_refill, launch_lone, launch_wavefront, launch_fast_screen};
 struct Registrar {
     Registrar() { register_experimental_kernels(&kTable); }
     ~Registrar() { register_experimental_kernels(nullptr); }

@@ -1138,240 +1138,6 @@ __device__ __forceinline__ void lone_traverse(const float4* nodes4, const float4
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// Lone-ray traversal through the treelets (MODE bit 7; mirror.h treelets / tlloc).  The same job
-// as lone_traverse -- one lane left in the small phase, the whole wave on its ray -- with the
-// lone-pixel kernel's walk (rt_lone.hip): a treelet holds up to 63 nodes in the DFS's right-first
-// preorder, one load round and one IEEE IntersectAABB per lane (Math.h:50-61) test all of them
-// at once, and the DFS inside is a few ballots per leaf -- a node is visited iff it and every
-// ancestor passed `tmax >= tmin && tmin < closest && tmax > 0` at the moment the reference popped
-// it (main_raytracing.cu:43-47): decisions before the walk's position are frozen, later ones use
-// the live closest distance.  How a lane's traversal maps onto it: the DFS finishes the subtree
-// of the node a lane stands at before it pops anything below, so
-//   * the node the lane stands at: its subtree is walked from the node's own treelet slot
-//     (tlloc, keyed by its first_index) -- or, a small leaf, tested;
-//   * then the lane's stack, lane j = entry j with its exact pop-time key: the highest entry that
-//     passes with the live closest distance is the one the reference's pops stop at, and its
-//     subtree is walked the same way;
-//   * a big leaf hands the ray back: the lane stands at the leaf and its stack is what the
-//     reference's would hold there -- the untouched entries below, then for every node on the
-//     walk's path whose right child the path took, that node's left child (mirror.h: an inner
-//     treelet slot's X), outermost first -- and the wave's big-leaf round takes over.
-// Small leaves: one triangle per lane, the (t, index) minimum below the entry closest distance
-// (lone_traverse).  Same visits, same decisions, bit for bit.
-// ---------------------------------------------------------------------------------------
-constexpr uint32_t TLT_EMPTY = 0xffffffffu;  // treelet slot without a node (mirror.h)
-
-struct TLLane {  // this lane's slot of the current treelet
-    float key;  // IntersectAABB's box part: tmin when tmax >= tmin && tmax > 0, else +inf
-    uint32_t x, cnt;
-    unsigned long long anc;  // ancestor slots
-    uint32_t size;           // subtree size in slots, itself included
-    uint32_t frontier;       // 1: an inner node whose subtree is another treelet (a word, not a per-lane
-                             // bool: a bool kept in a lane mask across the walk's loops mis-rendered
-                             // frames of the 6-wave build, as screen_leaf's did -- Trav::sp)
-};
-
-__device__ __forceinline__ void tlt_load(const float4* tl, uint32_t t, uint32_t lane, const Ray& U, TLLane& s) {
-    const float4* p = tl + (size_t)t * 192u + 3u * lane;
-    const float4 lo = p[0], hi = p[1], g = p[2];
-    s.cnt = __float_as_uint(hi.w);
-    s.x = __float_as_uint(hi.z);
-    s.anc = (unsigned long long)__float_as_uint(g.x) | ((unsigned long long)__float_as_uint(g.y) << 32);
-    s.size = __float_as_uint(g.z);
-    s.frontier = __float_as_uint(g.w);
-    s.key = __int_as_float(0x7f800000);
-    if (s.cnt != TLT_EMPTY) {
-        float tmin, tmax;
-        slab_exact(U, lo, hi, &tmin, &tmax);
-        if (tmax >= tmin && tmax > 0.0f) s.key = tmin;
-    }
-}
-
-__device__ __forceinline__ unsigned long long tlt_bits(uint32_t lo, uint32_t hi) {  // [lo, hi), hi <= 64
-    const unsigned long long top = hi >= 64u ? ~0ull : ((1ull << hi) - 1ull);
-    const unsigned long long bot = lo >= 64u ? ~0ull : ((1ull << lo) - 1ull);
-    return top & ~bot;
-}
-
-// A small leaf [cf, cf + cc) for the wave-uniform ray: one triangle per lane, (t, index) minimum.
-__device__ __forceinline__ void lone_small_leaf(const float4* tris, int lane, uint32_t cf, uint32_t cc, const Ray& U,
-                                                float& best, int& kind, uint32_t& id, float& bx, float& by) {
-    float t = 0.0f, x = 0.0f, y = 0.0f;
-    bool nan = false, acc = false;
-    if ((uint32_t)lane < cc) {
-        const uint32_t i = cf + (uint32_t)lane;
-        acc = tri_accept(U.o, U.nd, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], best, &t, &x, &y, &nan);
-    }
-    if (__ballot(nan)) {  // the sequential loop (never taken for finite scenes)
-        if (lane == 0) {
-            for (uint32_t i = cf; i < cf + cc; i++) {
-                float tt, xx, yy;
-                bool dummy = false;
-                if (tri_accept(U.o, U.nd, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], best, &tt, &xx, &yy, &dummy))
-                    best = tt, kind = 2, bx = xx, by = yy, id = __float_as_uint(tris[3 * i + 2].y);
-            }
-        }
-        best = bcast(best, 0), kind = __builtin_amdgcn_readlane(kind, 0), id = bcastu(id, 0);
-        bx = bcast(bx, 0), by = bcast(by, 0);
-    } else if (__ballot(acc)) {
-        const uint32_t mk = __ockl_wfred_min_u32(acc ? tkey(t) : 0xffffffffu);
-        const uint32_t mi = __ockl_wfred_min_u32(acc && tkey(t) == mk ? (uint32_t)lane : 0xffffffffu);
-        const int wl = (int)mi;
-        best = bcast(t, wl), bx = bcast(x, wl), by = bcast(y, wl), kind = 2;
-        id = __float_as_uint(tris[3 * (cf + mi) + 2].y);
-    }
-}
-
-template <int SL>
-__device__ __forceinline__ void lone_treelet(const float4* nodes4, const float4* tris, const float4* tl,
-                                             const uint32_t* tlloc, const Stack<SL>& stk, int r, const Ray& R, Hit& h,
-                                             Trav& T, bool& active) {
-    const int lane = (int)(threadIdx.x & 63u);
-    uint32_t* const col = stk.lds - lane + r;  // lane r's LDS stack column
-    int sp = (int)bcastu((uint32_t)T.sp, r);
-    uint32_t cf = bcastu(T.first, r), cc = bcastu(T.count, r);
-    Ray U;  // the lone ray, wave-uniform
-    U.o = bcast3(R.o, r), U.d = bcast3(R.d, r), U.nd = bcast3(R.nd, r), U.r = bcast3(R.r, r);
-    U.fast = false;
-    float best = bcast(h.best, r);
-    int kind = __builtin_amdgcn_readlane(h.kind, r);
-    uint32_t id = bcastu(h.id, r);
-    float bx = bcast(h.bx, r), by = bcast(h.by, r);
-    const float inf = __int_as_float(0x7f800000);
-    // the lane's stack, lane j = entry j: the pop-time IntersectAABB key, first, count
-    float e_key = inf;
-    uint32_t e_first = 0, e_count = 0;
-    if (lane < sp) {
-        const uint32_t idx = col[lane * WAVE];
-        const float4 lo = nodes4[2 * idx], hi = nodes4[2 * idx + 1];
-        float tmin, tmax;
-        slab_exact(U, lo, hi, &tmin, &tmax);
-        if (tmax >= tmin && tmax > 0.0f) e_key = tmin;
-        e_first = __float_as_uint(hi.z), e_count = __float_as_uint(hi.w);
-    }
-    // suspended frames of nested treelets: lane d of fT / fEC / fZl / fZh holds frame d (treelet,
-    // entry slot | next slot << 8, frozen decisions)
-    int fT = 0, fEC = 0, fZl = 0, fZh = 0;
-    bool handed = false;
-    for (;;) {
-        if (cc == 0) {
-            // the subtree of inner node (cf = its first_index), walked from its treelet slot
-            const uint32_t loc = __builtin_amdgcn_readfirstlane((int)tlloc[cf]);
-            uint32_t tt = loc >> 6, e = loc & 63u, cur = e + 1u;
-            unsigned long long fz = 0ull;
-            int depth = 0;
-            TLLane s;
-            tlt_load(tl, tt, (uint32_t)lane, U, s);
-            for (;;) {
-                const uint32_t esize = bcastu(s.size, (int)e);
-                const unsigned long long in_sub = tlt_bits(e + 1u, e + esize);
-                const unsigned long long below = tlt_bits(0u, cur);
-                const unsigned long long live = __ballot(s.key < best);
-                const unsigned long long pm = (fz & below) | (live & ~below);
-                const bool blocked = (s.anc & in_sub & ~pm) != 0ull;
-                const bool is_event = s.cnt != TLT_EMPTY && (s.cnt > 0u || s.frontier != 0u);
-                const unsigned long long ev =
-                    __ballot(((in_sub & ~below & pm) >> lane & 1ull) != 0ull && is_event && !blocked);
-                if (!ev) {
-                    if (depth == 0) break;
-                    depth--;  // back to the treelet this one hangs from, after its frontier
-                    tt = (uint32_t)__builtin_amdgcn_readlane(fT, depth);
-                    const uint32_t ec = (uint32_t)__builtin_amdgcn_readlane(fEC, depth);
-                    e = ec & 255u, cur = ec >> 8;
-                    fz = (unsigned long long)(uint32_t)__builtin_amdgcn_readlane(fZl, depth) |
-                         ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(fZh, depth) << 32);
-                    tlt_load(tl, tt, (uint32_t)lane, U, s);
-                    continue;
-                }
-                const uint32_t nr = (uint32_t)__ffsll((long long)ev) - 1u;
-                fz = (fz & below) | (pm & tlt_bits(cur, nr + 1u));  // the decisions up to the event are made
-                cur = nr + 1u;
-                const uint32_t ex = bcastu(s.x, (int)nr), ec = bcastu(s.cnt, (int)nr);
-                if (ec == 0u) {  // a frontier: its subtree is treelet ex, entered at its root (slot 0)
-                    if (lane == depth) {
-                        fT = (int)tt, fEC = (int)(e | (cur << 8));
-                        fZl = (int)(uint32_t)fz, fZh = (int)(uint32_t)(fz >> 32);
-                    }
-                    depth++;
-                    tt = ex, e = 0u, cur = 1u, fz = 0ull;
-                    tlt_load(tl, tt, (uint32_t)lane, U, s);
-                } else if (ec <= (uint32_t)BIG) {
-                    lone_small_leaf(tris, lane, ex, ec, U, best, kind, id, bx, by);
-                } else {
-                    // a big leaf: the reference's stack at this leaf, outermost frame first
-                    for (int k = 0; k <= depth; k++) {
-                        uint32_t tk, sk, gk;
-                        unsigned long long anc;
-                        if (k < depth) {
-                            tk = (uint32_t)__builtin_amdgcn_readlane(fT, k);
-                            const uint32_t eck = (uint32_t)__builtin_amdgcn_readlane(fEC, k);
-                            sk = eck & 255u, gk = (eck >> 8) - 1u;  // entry slot, its frontier event
-                            const f4v G = ((ConstF4)tl)[(size_t)tk * 192u + 3u * gk + 2u];
-                            anc = (unsigned long long)__float_as_uint(G.x) | ((unsigned long long)__float_as_uint(G.y) << 32);
-                        } else {
-                            tk = tt, sk = e, gk = nr;
-                            anc = (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)s.anc, (int)nr) |
-                                  ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(s.anc >> 32), (int)nr) << 32);
-                        }
-                        const unsigned long long onpath = anc | (1ull << gk);
-                        for (unsigned long long A = anc & tlt_bits(sk, gk); A; A &= A - 1ull) {
-                            const uint32_t a = (uint32_t)__ffsll((long long)A) - 1u;
-                            if ((onpath >> (a + 1u)) & 1ull) {  // the path took a's right child (slot a + 1)
-                                const uint32_t left = k < depth ? __float_as_uint(((ConstF4)tl)[(size_t)tk * 192u + 3u * a + 1u].z)
-                                                                : bcastu(s.x, (int)a);
-                                if (lane == r) stk.put(sp, left);
-                                sp++;
-                            }
-                        }
-                    }
-                    cf = ex, cc = ec;
-                    handed = true;
-                    break;
-                }
-            }
-            if (handed) break;
-        } else {
-            lone_small_leaf(tris, lane, cf, cc, U, best, kind, id, bx, by);
-        }
-        // pop: the highest entry that passes with the live closest distance (the ones above it fail)
-        const unsigned long long m = __ballot(lane < sp && e_key < best);
-        if (!m) {
-            sp = 0;
-            break;
-        }
-        const int j = 63 - __clzll((long long)m);
-        cf = bcastu(e_first, j), cc = bcastu(e_count, j);
-        sp = j;
-        if (cc > (uint32_t)BIG) {  // a big leaf: entries 0 .. j - 1 stay as they are
-            handed = true;
-            break;
-        }
-    }
-    if (lane == r) {
-        h.best = best, h.kind = kind, h.id = id, h.bx = bx, h.by = by;
-        T.first = cf, T.count = cc, T.sp = sp;
-        active = handed;
-    }
-}
-
-// lone_treelet as a call of its own: its registers (treelet slot, frames, stack keys, the uniform ray)
-// stay out of the render loop's allocation (inlined, the 7-wave config-2 kernel ran 26.7 instead of
-// 14.8 ms with the walk compiled in but never taken).
-struct LoneResult {
-    Hit h;
-    Trav T;
-    uint32_t active;
-};
-template <int SL>
-__device__ __noinline__ LoneResult lone_treelet_call(const float4* nodes4, const float4* tris, const float4* tl,
-                                                     const uint32_t* tlloc, Stack<SL> stk, int r, Ray R, Hit h, Trav T,
-                                                     uint32_t active) {
-    bool a = active != 0u;
-    lone_treelet(nodes4, tris, tl, tlloc, stk, r, R, h, T, a);
-    return LoneResult{h, T, a ? 1u : 0u};
-}
-
 // BVHRayHit for one lane (`live` = the lane has a segment to trace), every lane of the wave
 // calling.  Small steps run while any lane has one; big leaves wait until every lane is done
 // or waiting at one.  MODE & 3 -- 0: big leaves through pair records (shared-leaf loop and
@@ -1382,8 +1148,7 @@ template <bool STATS, int MODE, class S, class C>
 __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, const float4* pairs,
                                       const float4* tree, const float4* ltris, const float4* flat,
                                       const float4* spairs, uint32_t tune, const S& stk, uint32_t* scratch,
-                                      const Ray& R, Hit& h, bool live, C& c, const float4* tl = nullptr,
-                                      const uint32_t* tlloc = nullptr) {
+                                      const Ray& R, Hit& h, bool live, C& c) {
     Trav T{0, 0, 0};
     bool active = live && trav_begin<STATS>(nodes4, R, h, T, c);
     // big-leaf screens (screen_leaf, MODE bit 5): split-step variants for scenes that have them
@@ -1413,12 +1178,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
 #ifdef RT_LANE_HIST  // diagnostic build (tools/lane_hist.sh): wave cycles of the lone-lane tails
                             const unsigned long long tl0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
 #endif
-                            if constexpr ((MODE & 128) != 0) {  // MODE bit 7: through the treelets
-                                const LoneResult o = lone_treelet_call(nodes4, tris, tl, tlloc, stk, r, R, h, T,
-                                                                       active ? 1u : 0u);
-                                h = o.h, T = o.T, active = o.active != 0u;
-                            } else
-                                lone_traverse(nodes4, tris, stk, r, R, h, T, active);
+                            lone_traverse(nodes4, tris, stk, r, R, h, T, active);
 #ifdef RT_LANE_HIST
                             if (TIMING) c.cy_ttri += __builtin_amdgcn_s_memtime() - tl0;
 #endif

@@ -223,7 +223,6 @@ std::atomic<const ExperimentalKernels*> g_experimental{nullptr};
 bool needs_experimental(const rt_render_params* p, bool has_tree, bool screens) {
     const bool stats = (p->flags & RT_RENDER_STATS) != 0;
     if ((p->flags & RT_RENDER_TRACER_WAVEFRONT) || p->refill_lanes || p->lone_count > 0) return true;
-    if ((p->tune & (1u << 20)) && (p->tune & 4096u) == 0 && (!stats || (p->tune & 256u))) return true;  // treelet lone walk
     if (screens && (p->tune & 4096u) == 0 && (!stats || (p->tune & 256u))) return true;  // big-leaf screen variants
     if (stats || p->lane_cost) return false;  // statistics / timing families are in the product
     const uint32_t mode = (p->tune >> 4) & 3u;
@@ -237,19 +236,13 @@ hipError_t launch_fast(const RenderArgs& args, int waves, int depth, bool stats,
     const ExperimentalKernels* x = g_experimental.load();  // rt_render refused these frames without it
     // MODE bit 5 (librt_hip_exp.so): big-leaf screens, for scenes whose mirror has screen records
     const bool scr = args.screens != 0 && (args.tune & 4096u) == 0;
-    // MODE bit 7 (librt_hip_exp.so, RT_TUNE bit 20): lone rays through the treelets; rt_render passes
-    // the treelet location table only then, so its variants of the split-step production and timing
-    // kernels run instead of the product's
-    const bool tlw = args.tlloc != nullptr && (args.tune & 4096u) == 0 && !scr && !args.queue_head;
     if (stats && (args.tune & 256u)) {
         if (scr) return x ? x->fast_screen(stack, args.tree ? 61 : 57, args, waves, s) : hipErrorNotSupported;
-        if (tlw) return x ? x->fast_tl(stack, args.tree ? 157 : 153, args, waves, s) : hipErrorNotSupported;
         return launch_fast_timing(stack, args.tree ? 29 : (args.tune & 4096u) ? 9 : 25, args, waves, s);
     }
     // per-pixel work (rt_render_params.lane_cost): the timing variant of the production kernel
     if (!stats && args.lane_cost) {
         if (scr) return x ? x->fast_screen(stack, args.tree ? 61 : 57, args, waves, s) : hipErrorNotSupported;
-        if (tlw) return x ? x->fast_tl(stack, args.tree ? 157 : 153, args, waves, s) : hipErrorNotSupported;
         return launch_fast_timing(stack, args.tree ? 29 : 25, args, waves, s);
     }
     if (stats) return launch_fast_stats(stack, (args.tree && (args.tune & 128u)) ? 6 : 2, args, waves, s);
@@ -261,8 +254,6 @@ hipError_t launch_fast(const RenderArgs& args, int waves, int depth, bool stats,
     if (args.queue_head) return x ? x->fast_refill(stack, args.tree ? 85 : 81, args, waves, s) : hipErrorNotSupported;
     if (scr && split && (args.tree || ((args.tune >> 4) & 3u) < 2u))
         return x ? x->fast_screen(stack, args.tree ? 53 : 49, args, waves, s) : hipErrorNotSupported;
-    if (tlw && (args.tree || ((args.tune >> 4) & 3u) < 2u))
-        return x ? x->fast_tl(stack, args.tree ? 149 : 145, args, waves, s) : hipErrorNotSupported;
     if (args.tree) {
         if (split) return launch_fast_prod(stack, 21, args, waves, s);
         return x ? x->fast_ab(stack, 5, args, waves, s) : hipErrorNotSupported;
@@ -466,8 +457,7 @@ void upload_mirror(ForeignBuild* b) {
         rt_build_mirror(nodes, b->bytes[0] / sizeof(GPUBVHNode), fi, b->bytes[1] / 4, faces, b->bytes[2] / sizeof(GPUFace),
                         verts, b->bytes[3] / sizeof(GPUVertex), &mh);
         const std::vector<float> lt = rt_ltris_device_layout(mh.ltris);
-        const std::vector<float>* parts[9] = {&mh.tris, &mh.pairs, &mh.tree, &lt, &mh.spairs, &mh.flat, &mh.treelets, &mh.nodes,
-                                              &mh.tlloc};
+        const std::vector<float>* parts[8] = {&mh.tris, &mh.pairs, &mh.tree, &lt, &mh.spairs, &mh.flat, &mh.treelets, &mh.nodes};
         size_t total = 256;  // each part on a 256-B boundary (mirror.h: cache-line aligned pairs)
         for (auto* v : parts) total += (v->size() * 4 + 255) & ~(size_t)255;
         hipStream_t st;
@@ -475,8 +465,8 @@ void upload_mirror(ForeignBuild* b) {
         void* block = nullptr;
         if (hipMallocAsync(&block, total, st) != hipSuccess) throw std::runtime_error("mirror allocation failed");
         char* p = static_cast<char*>(block);
-        const void* where[9];
-        for (int i = 0; i < 9; i++) {
+        const void* where[8];
+        for (int i = 0; i < 8; i++) {
             const size_t nb = parts[i]->size() * 4;
             where[i] = nb ? p : nullptr;
             if (nb && hipMemcpyAsync(p, parts[i]->data(), nb, hipMemcpyHostToDevice, st) != hipSuccess)
@@ -489,7 +479,6 @@ void upload_mirror(ForeignBuild* b) {
         b->block = block;
         b->dev.tris = where[0], b->dev.pairs = where[1], b->dev.tree = where[2], b->dev.ltris = where[3];
         b->dev.spairs = where[4], b->dev.flat = where[5], b->dev.treelets = where[6], b->dev.nodes = where[7];
-        b->dev.tlloc = where[8];
         b->dev.depth = mh.depth, b->dev.fast = mh.fast, b->dev.owned = false, b->dev.fingerprint = b->fingerprint;
         b->dev.screens = mh.screens;
         b->state = 2;
@@ -834,13 +823,6 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     // reference-layout tracers keep the reference's
     const GPUBVHNode* const trav_nodes =
         (mir.nodes && (a.tune & (1u << 27)) == 0) ? (const GPUBVHNode*)mir.nodes : scene->gpu_bvh_nodes;
-    // RT_TUNE bit 20: lone rays through the treelets (MODE bit 7), which need the private node array
-    // (tlloc is keyed by its slots) and a BVH whose treelet nesting fits a wave's lanes
-    if ((a.tune & (1u << 20)) && mir.treelets && mir.tlloc && trav_nodes == (const GPUBVHNode*)mir.nodes && depth >= 0 &&
-        depth <= 62 && (!stats || (a.tune & 256u))) {
-        a.treelets = (const float4*)mir.treelets;
-        a.tlloc = (const uint32_t*)mir.tlloc;
-    }
     auto trav = [&](const RenderArgs& x) {  // the arguments as they stand at launch, traversal nodes
         RenderArgs f = x;
         f.nodes = trav_nodes;

@@ -23,7 +23,6 @@ hipError_t launch_ref_tracer(bool flat, const RenderArgs& a, int waves, int dept
 hipError_t launch_fast_ab(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);      // 1, 5, 2, 0
 hipError_t launch_fast_refill(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);  // 81, 85
 hipError_t launch_fast_screen(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);  // 49, 53, 57, 61
-hipError_t launch_fast_tl(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);      // 145, 149, 153, 157
 // The lone-pixel kernel (rt_lone.hip): one wave per slot of `lone_slots`, through the treelets.
 hipError_t launch_lone(const RenderArgs& a, const int32_t* lone_slots, int lone_count, const void* treelets, hipStream_t s);
 // The wavefront tracer (rt_wavefront.hip): shade / trace launches per segment generation.
@@ -35,7 +34,6 @@ struct ExperimentalKernels {
     decltype(&launch_lone) lone;
     decltype(&launch_wavefront) wavefront;
     decltype(&launch_fast_screen) fast_screen;
-    decltype(&launch_fast_tl) fast_tl;
 };
 // rt_kernel.hip: the registered table (nullptr until librt_hip_exp.so is loaded).
 void register_experimental_kernels(const ExperimentalKernels* k);

@@ -715,15 +715,6 @@ int rt_scene_mirror_nodes(rt_scene* s, GPUBVHNode* nodes, size_t* count) {
     if (nodes) std::memcpy(nodes, m.nodes.data(), m.nodes.size() * 4);
     return 0;
 }
-int rt_scene_mirror_treelets(rt_scene* s, float* treelets, size_t* treelet_count, uint32_t* tlloc, size_t* tlloc_count) {
-    MirrorHost m;
-    if (host_mirror(s, &m) != 0) return -1;
-    *treelet_count = m.treelets.size() / (64 * 12);
-    *tlloc_count = m.tlloc.size();
-    if (treelets) std::memcpy(treelets, m.treelets.data(), m.treelets.size() * 4);
-    if (tlloc) std::memcpy(tlloc, m.tlloc.data(), m.tlloc.size() * 4);
-    return 0;
-}
 void rt_scene_build(rt_scene* s) { s->scene.BuildHost(); }
 void rt_scene_camera(const rt_scene* s, GPUCamera* out) {
     *out = static_cast<const GPUCamera&>(const_cast<Scene&>(s->scene).GetCamera());

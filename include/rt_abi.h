@@ -483,11 +483,6 @@ int rt_cluster_cull_host(const float origin[3], const float nd[3], float best, c
    aligned in right-first pre-order), built on the host: *count receives the node count; nodes (may
    be NULL) receives the records.  0 or -1 with rt_last_error(). */
 int rt_scene_mirror_nodes(rt_scene* scene, GPUBVHNode* nodes, size_t* count);
-/* The treelets (mirror.h treelets: 64 slots x 12 floats each) and the treelet location of every
-   inner node by its private first_index (mirror.h tlloc: treelet << 6 | slot, ~0u elsewhere), built
-   on the host: counts first, then the arrays when the pointers are not NULL.  0 or -1. */
-int rt_scene_mirror_treelets(rt_scene* scene, float* treelets, size_t* treelet_count, uint32_t* tlloc,
-                             size_t* tlloc_count);
 
 /* XORWOW jump matrix A^(4^k * 2^67) (k < 32) as 800 uint32 words in rocrand's layout
  * m[i*160 + j*5 + w] (input word i, bit j, output word w).  For tests. */

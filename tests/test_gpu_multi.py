@@ -525,61 +525,3 @@ def test_lone_misuse_is_refused(rt):
     with pytest.raises(rt.RTError, match="production tracer"):
         rt.render(s, a, b, w, h, 1, 1, tracer="ref", lone_slots=lo, lane_slots=torch.full((64,), -1, dtype=torch.int32, device="cuda"))
     torch.cuda.synchronize()
-
-
-def sparse_lane_map(rt, w, h, per_wave):
-    """Every tile in order, `per_wave` pixels to a wave (the rest of its lanes idle): waves whose
-    lanes finish one by one, so most of their traversal steps run with a lone lane left."""
-    slots = np.arange(rt.sharding.tiles_total(w, h) * 256, dtype=np.int64)
-    waves = (slots.size + per_wave - 1) // per_wave
-    m = np.full((waves, 64), -1, dtype=np.int32)
-    for k in range(per_wave):
-        part = slots[k::per_wave]
-        m[: part.size, k] = part
-    return torch.from_numpy(m.reshape(-1)).cuda()
-
-
-@pytest.mark.parametrize("which,wps", [("bunny", 7), ("bunny", 5), ("bunny4", 5), ("bunny4", 6)])
-def test_treelet_lone_walk_equal_plain(rt, which, wps):
-    """Lone rays walked through the treelets (RT_TUNE bit 20, MODE bit 7, rt_fast.h lone_treelet:
-    subtree walks by ballots over treelet slots, the stack's pop-time keys in lanes, big leaves handed
-    back with the reference's stack) render the frame and RNG states bit for bit as the production
-    kernel's lone_traverse, with the plain order and with 1- and 3-pixel waves (most steps lone)."""
-    w, h, spp, bounces = 128, 72, 2, 6
-    mine = torch.arange(rt.sharding.tiles_total(w, h), dtype=torch.int32, device="cuda")
-    for lanes in (None, 1, 3):
-        res = {}
-        for tune in (0, 1 << 20):
-            s = scene(rt, w, h, which)
-            rng = rt.alloc_rng(w * h)
-            rt.init_rng_states(rng, w, h, T.SEED)
-            s.upload(rng.data_ptr())
-            a, b = rt.alloc_surface(w, h), rt.alloc_surface(w, h)
-            lm = sparse_lane_map(rt, w, h, lanes) if lanes else None
-            for f in range(2):
-                rt.render(s, (a, b)[f], (b, a)[f], w, h, spp, bounces, f, tile_list=mine if lm is not None else None,
-                          lane_slots=lm, waves_per_simd=wps, tune=tune)
-            torch.cuda.synchronize()
-            res[tune] = (rt.surface_view(b, w).cpu().numpy().copy(), rng.cpu().numpy().copy())
-        assert np.array_equal(res[0][0].view(np.uint32), res[1 << 20][0].view(np.uint32)), (which, wps, lanes)
-        assert np.array_equal(res[0][1], res[1 << 20][1]), (which, wps, lanes)
-
-
-def test_treelet_lone_walk_timing_frame_equal(rt):
-    """The timing variant with the treelet walk (what bench.py's probe and refinement frames run
-    under RT_TUNE bit 20) renders the same frame as the production kernel."""
-    w, h, spp, bounces = 128, 72, 2, 6
-    out = {}
-    for tune, cost in ((0, False), (1 << 20, True)):
-        s = scene(rt, w, h, "bunny4")
-        rng = rt.alloc_rng(w * h)
-        rt.init_rng_states(rng, w, h, T.SEED)
-        s.upload(rng.data_ptr())
-        a, b = rt.alloc_surface(w, h), rt.alloc_surface(w, h)
-        mine = torch.arange(rt.sharding.tiles_total(w, h), dtype=torch.int32, device="cuda")
-        lc = torch.zeros(mine.numel() * 256, dtype=torch.int32, device="cuda") if cost else None
-        rt.render(s, a, b, w, h, spp, bounces, 0, tile_list=mine if cost else None, lane_cost=lc, tune=tune)
-        torch.cuda.synchronize()
-        out[tune] = (rt.surface_view(a, w).cpu().numpy().copy(), rng.cpu().numpy().copy())
-    assert np.array_equal(out[0][0].view(np.uint32), out[1 << 20][0].view(np.uint32))
-    assert np.array_equal(out[0][1], out[1 << 20][1])

@@ -162,44 +162,3 @@ def _big_leaf_flags(rt, which):
         nodes = s.host_arrays()["nodes"].view(np.uint32).reshape(-1, 8)
         big = nodes[(nodes[:, 7] > 8)]
         return {int(n[7]): int(tris[n[6], 11]) for n in big}
-
-
-@pytest.mark.parametrize("which", ["bunny", "bunny4"])
-def test_treelet_locations(which):
-    """mirror.h tlloc / treelets for the treelet lone walk (rt_fast.h lone_treelet): every inner node
-    of the private array has exactly one treelet slot that holds it with its children (keyed by its
-    first_index), that slot has the node's box, X = first_index (the left child the reference's DFS
-    pushes), the right child at the next slot and the left child after the right child's subtree;
-    frontier slots point at a treelet whose slot 0 is the same node."""
-    rt = T.load_rt()
-    s = rt.Scene()
-    s.setup(which)
-    s.build()
-    prv = s.mirror_nodes()
-    prvu = prv.view(np.uint32)
-    tl, loc = s.mirror_treelets()
-    tlu = tl.view(np.uint32)
-    assert loc.size == prv.shape[0]
-    inner = [b for b in range(prv.shape[0]) if b != 1 and prvu[b, 7] == 0]
-    firsts = {int(prvu[b, 6]): b for b in inner}
-    assert len(firsts) == len(inner)
-    keyed = np.nonzero(loc != 0xFFFFFFFF)[0]
-    assert set(int(k) for k in keyed) == set(firsts), "a location for exactly the inner nodes' first_index"
-    for f, b in firsts.items():
-        t, slot = int(loc[f]) >> 6, int(loc[f]) & 63
-        rec = tlu[t, slot]
-        assert np.array_equal(tl[t, slot, :6].view(np.uint32), prv[b, :6].view(np.uint32)), (b, t, slot)
-        assert rec[7] == 0 and rec[11] == 0 and rec[6] == f, "an expanded inner slot: X = first_index"
-        right = slot + 1
-        left = right + int(tlu[t, right, 10])
-        assert np.array_equal(tl[t, right, :6].view(np.uint32), prv[f + 1, :6].view(np.uint32))
-        assert np.array_equal(tl[t, left, :6].view(np.uint32), prv[f, :6].view(np.uint32))
-        assert int(rec[10]) == 1 + int(tlu[t, right, 10]) + int(tlu[t, left, 10])
-        anc_r = int(tlu[t, right, 8]) | (int(tlu[t, right, 9]) << 32)
-        assert (anc_r >> slot) & 1, "the node is an ancestor of its right child"
-    for t in range(tl.shape[0]):
-        for slot in range(64):
-            if tlu[t, slot, 7] == 0 and tlu[t, slot, 11] == 1:  # a frontier
-                c = int(tlu[t, slot, 6])
-                assert np.array_equal(tl[c, 0, :6].view(np.uint32), tl[t, slot, :6].view(np.uint32))
-                assert tlu[c, 0, 11] == 0 and tlu[c, 0, 7] == 0
