@@ -21,6 +21,7 @@ tunes = [int(x, 0) for x in (sys.argv[4] if len(sys.argv) > 4 else "0").split()]
 occs = [int(x) for x in (sys.argv[5] if len(sys.argv) > 5 else "5 6 7").split()]
 spp = int(os.environ.get("SPP", "4"))
 rt = T.load_rt()
+rt.load_experimental()  # A/B variants (librt_hip_exp.so)
 if os.environ.get("BUILD_OPTS"):  # e.g. "leaf_screens=0" (rt_set_build_options)
     rt.set_build_options(**{k: float(v) if k == "split_angle" else int(v)
                             for k, v in (kv.split("=") for kv in os.environ["BUILD_OPTS"].split(","))})
@@ -38,9 +39,11 @@ for t in tunes:
         rt.render(s, out, last, w, h, spp, 6, 0, waves_per_simd=o, tune=t)
         torch.cuda.synchronize()
         res.append(((t, o), rt.surface_view(out, w).cpu().numpy().copy(), rng.view(-1, 12)[:, :6].cpu().numpy().copy()))
+if os.environ.get("ORACLE"):  # the CPU oracle's frame first (the reference for every combination)
+    res.insert(0, (("oracle", 0), T.OracleScene(which).render(w, h, spp, 6), None))
 _, b_img, b_st = res[0]
 for k, img, st in res:
     diff = np.flatnonzero((img.view(np.uint32) != b_img.view(np.uint32)).any(-1).ravel())
-    print(json.dumps({"scene": which, "tune": hex(k[0]), "wps": k[1], "pixels_differ": int(diff.size),
-                      "rng_differ": int((st != b_st).any(-1).sum()),
+    print(json.dumps({"scene": which, "tune": k[0] if isinstance(k[0], str) else hex(k[0]), "wps": k[1], "pixels_differ": int(diff.size),
+                      "rng_differ": int((st != b_st).any(-1).sum()) if st is not None and b_st is not None else None,
                       "first": [[int(p % w), int(p // w)] for p in diff[:5]]}), flush=True)
