@@ -156,6 +156,7 @@ SIGNATURES = {
     "rt_scene_mirror_copy": (_I, [_P, _P, _P, _P]),
     "rt_scene_mirror_nodes": (_I, [_P, _P, ctypes.POINTER(_SZ)]),
     "rt_cluster_cull_host": (_I, [_P, _P, ctypes.c_float, _P]),
+    "rt_twin_check_host": (_I, [_P, _P, _P]),
     "rt_xorwow_jump_matrix": (_I, [_I, ctypes.POINTER(ctypes.c_uint32)]),
     "rt_xorwow_init_host": (None, [_U32, _U64, _P]),
 }

@@ -31,6 +31,11 @@ FP_FLAGS = ["-ffp-contract=off", "-fno-fast-math"]
 # structurized like divergent ones (config 2: 15.65 vs 15.93 ms per frame, three interleaved runs
 # on one box, tools/build_variant.sh + tools/gpu_variants.sh; config 4 unchanged).
 HIP_CODEGEN_FLAGS = ["-mllvm", "-structurizecfg-skip-uniform-regions=1"]
+# ... except for the 6-wave kernels: each render family below is compiled twice, once with the option
+# and its 6-wave kernels sent to a second unit (RT_W6_SPLIT), once without the option holding only those
+# (RT_W6_ONLY) -- the 6-wave leaf-tree kernel was miscompiled under the option (rt_fast_body.h)
+W6_SPLIT = {"rt_fast_prod.hip", "rt_fast_timing.hip", "rt_fast_ab.hip", "rt_fast_ab2.hip", "rt_fast_refill.hip",
+            "rt_fast_screen.hip"}
 HOST_SOURCES = ["scene.cpp", "objload.cpp", "mirror.cpp", "leaftree.cpp", "xorwow.cpp", "image.cpp", "shard.cpp"]
 # the render kernel families compile as separate translation units, in parallel (rt_render.h)
 HIP_SOURCES = ["rt_fast_prod.hip", "rt_fast_timing.hip", "rt_fast_stats.hip", "rt_ref.hip", "rt_kernel.hip", "image.hip",
@@ -59,11 +64,17 @@ def _deps(dirpath, exts):
     return [os.path.join(dirpath, f) for f in os.listdir(dirpath) if f.endswith(exts)]
 
 
-def _hip_job(src):
-    obj = os.path.join(BUILD, src + ".o")
+def _hip_job(src, w6=None):
+    """w6: None (a plain unit), "split" (RT_W6_SPLIT) or "only" (RT_W6_ONLY, without the codegen option)."""
+    obj = os.path.join(BUILD, src + (".w6.o" if w6 == "only" else ".o"))
+    extra = {None: HIP_CODEGEN_FLAGS, "split": HIP_CODEGEN_FLAGS + ["-DRT_W6_SPLIT"], "only": ["-DRT_W6_ONLY"]}[w6]
     return obj, [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *FP_FLAGS,
-                 "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics", "-fno-slp-vectorize", *HIP_CODEGEN_FLAGS,
+                 "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics", "-fno-slp-vectorize", *extra,
                  "-I", INC, "-I", CSRC, "-c", os.path.join(CSRC, src), "-o", obj]
+
+
+def _hip_jobs(src):
+    return [_hip_job(src, "split"), _hip_job(src, "only")] if src in W6_SPLIT else [_hip_job(src)]
 
 
 def _compile(jobs, force):
@@ -94,12 +105,12 @@ def _compile(jobs, force):
 def build_product(force=False):
     """librt_hip.so and the experimental plugin librt_hip_exp.so (linked against it)."""
     os.makedirs(BUILD, exist_ok=True)
-    jobs = [_hip_job(src) for src in HIP_SOURCES]
+    jobs = [j for src in HIP_SOURCES for j in _hip_jobs(src)]
     for src in HOST_SOURCES:
         obj = os.path.join(BUILD, src + ".o")
         jobs.append((obj, ["g++", "-O2", "-std=c++17", "-fPIC", *FP_FLAGS, "-I", INC, "-I", CSRC,
                            "-c", os.path.join(CSRC, src), "-o", obj]))
-    exp_jobs = [_hip_job(src) for src in EXP_SOURCES]
+    exp_jobs = [j for src in EXP_SOURCES for j in _hip_jobs(src)]
     changed = _compile(jobs + exp_jobs, force)
     objs = [o for o, _ in jobs]
     if changed or not _newer(LIB, objs):

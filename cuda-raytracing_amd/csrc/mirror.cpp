@@ -33,6 +33,99 @@ void put_pair(float* q, const float* a, const float* b) {
 }
 }  // namespace
 
+// Error bounds of glm::intersectRayTriangle's fp32 evaluation (gtx/intersect.inl:29-94, the operation
+// order of rt_fast.h test_triangle) for a triangle A = (v0, e1, e2) and its twin A' = (v0, e2, e1),
+// with U = 2^-24 and round-to-nearest, every product / sum rounding once:
+//   cross component: |c - c_R| <= (2U + U^2) T, T = the sum of the two products' magnitudes;
+//   3-term dot with computed second operand y: |d - x.y_R| <= gamma_3 sum |x_i y_i| + sum |x_i| |dy_i|.
+// det = e1.(nd x e2): |det - det_R| <= 5.000001 U S, S = sum over distinct (i, j, k) of |e1_i nd_j e2_k|
+// <= |e1|_1 |e2|_1 (|nd_j| <= 1 + 3U); S is symmetric in e1 and e2, and det'_R = -det_R exactly, so
+// |det + det'| <= 10.0001 U |e1|_1 |e2|_1 = kd.  With dist = o - v0 (the same computed value for both):
+// u = dist.(nd x e2) and v' = nd.(dist x e2) satisfy v'_R = -u_R, each within 5.000003 U |dist|_1 |e2|_1,
+// so |u + v'| <= 10.00001 U |dist|_1 |e2|_1; likewise |v + u'| <= 10.00001 U |dist|_1 |e1|_1.  ke =
+// 10.0001 U max(|e1|_1, |e2|_1), so ke |dist|_1 bounds both.  Computed in double, then widened by
+// 2^-20 before rounding to float (tests/test_scene.py checks the bound on sampled rays).
+void rt_twin_bounds(const float* r, float* kd, float* ke) {
+    const double U = std::ldexp(1.0, -24);
+    const double n1 = std::fabs((double)r[3]) + std::fabs((double)r[4]) + std::fabs((double)r[5]);
+    const double n2 = std::fabs((double)r[6]) + std::fabs((double)r[7]) + std::fabs((double)r[8]);
+    const double w = 1.0 + std::ldexp(1.0, -20);
+    *kd = (float)(10.0001 * U * n1 * n2 * w * w);
+    *ke = (float)(10.0001 * U * std::max(n1, n2) * w * w);
+}
+
+namespace {
+// The twins of big leaf [first, first + count) (mirror.h quads / units): units in leaf order, each a
+// triangle and (when the leaf holds one) its twin -- same v0, e1 and e2 swapped, bit for bit; a quad
+// packs two units.  Appends the leaf's quads and units; returns false (nothing appended) for a leaf
+// whose positions do not fit 16 bits.
+bool build_twins(const float* tris, uint32_t first, uint32_t count, std::vector<float>& quads,
+                 std::vector<float>& units, uint32_t* nq, uint32_t* nu) {
+    if (count >= 0xffffu) return false;
+    auto key = [&](uint32_t i, bool swapped) {
+        const float* r = &tris[(size_t)(first + i) * 12];
+        std::string k(reinterpret_cast<const char*>(r), 12);
+        k.append(reinterpret_cast<const char*>(r + (swapped ? 6 : 3)), 12);
+        k.append(reinterpret_cast<const char*>(r + (swapped ? 3 : 6)), 12);
+        return k;
+    };
+    std::map<std::string, std::vector<uint32_t>> by;
+    for (uint32_t i = 0; i < count; i++) by[key(i, false)].push_back(i);
+    std::vector<char> used(count, 0);
+    std::vector<std::pair<uint32_t, uint32_t>> un;  // (position, twin position or ~0u)
+    for (uint32_t i = 0; i < count; i++) {
+        if (used[i]) continue;
+        used[i] = 1;
+        uint32_t twin = ~0u;
+        auto it = by.find(key(i, true));
+        if (it != by.end())
+            for (uint32_t j : it->second)
+                if (!used[j]) {
+                    twin = j;
+                    used[j] = 1;
+                    break;
+                }
+        un.push_back({i, twin});
+    }
+    static const float zero[12] = {};
+    const uint32_t none = ~0u;
+    auto face = [&](uint32_t pos) { return pos == none ? none : *reinterpret_cast<const uint32_t*>(&tris[(size_t)(first + pos) * 12 + 9]); };
+    auto packed = [&](uint32_t pos, uint32_t twin) { return (pos & 0xffffu) | ((twin == none ? 0xffffu : twin) << 16); };
+    for (const auto& [pos, twin] : un) {  // units: 16 floats
+        float q[16] = {};
+        std::memcpy(q, &tris[(size_t)(first + pos) * 12], 10 * 4);
+        const uint32_t ft = face(twin), w = packed(pos, twin);
+        std::memcpy(&q[10], &ft, 4);
+        std::memcpy(&q[11], &w, 4);
+        rt_twin_bounds(&tris[(size_t)(first + pos) * 12], &q[12], &q[13]);
+        if (twin == none) q[12] = -1.0f;
+        units.insert(units.end(), q, q + 16);
+    }
+    for (size_t u = 0; u < un.size(); u += 2) {  // quads: 28 floats
+        const bool hb = u + 1 < un.size();
+        const float* ra = &tris[(size_t)(first + un[u].first) * 12];
+        const float* rb = hb ? &tris[(size_t)(first + un[u + 1].first) * 12] : zero;
+        float q[28] = {};
+        put_pair(q, ra, rb);
+        float kd, ke;
+        rt_twin_bounds(ra, &kd, &ke);
+        q[20] = un[u].second == none ? -1.0f : kd, q[22] = ke;
+        rt_twin_bounds(rb, &kd, &ke);
+        q[21] = (!hb || un[u + 1].second == none) ? -1.0f : kd, q[23] = ke;
+        const uint32_t wa = packed(un[u].first, un[u].second), wb = hb ? packed(un[u + 1].first, un[u + 1].second) : none;
+        const uint32_t fa = face(un[u].second), fb = hb ? face(un[u + 1].second) : none;
+        std::memcpy(&q[24], &wa, 4);
+        std::memcpy(&q[25], &wb, 4);
+        std::memcpy(&q[26], &fa, 4);
+        std::memcpy(&q[27], &fb, 4);
+        quads.insert(quads.end(), q, q + 28);
+    }
+    *nq = (uint32_t)((un.size() + 1) / 2);
+    *nu = (uint32_t)un.size();
+    return true;
+}
+}  // namespace
+
 void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t* fi, size_t index_count,
                      const GPUFace* faces, size_t face_count, const GPUVertex* verts, size_t vertex_count,
                      MirrorHost* out) {
@@ -48,6 +141,8 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
 
     // walk the tree from the root: depth, filtered-slab range, big leaves
     out->pairs.clear();
+    out->quads.clear();
+    out->units.clear();
     out->tree.clear();
     out->ltris.clear();
     out->flat.clear();
@@ -131,6 +226,17 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
             put_pair(q, &out->tris[((size_t)nd.first_index + j) * 12],
                      j + 1 < nd.prim_count ? &out->tris[((size_t)nd.first_index + j + 1) * 12] : nullptr);
             out->pairs.insert(out->pairs.end(), q, q + 20);
+        }
+        // the twins; the leaf's second / third record say where its quads / units are (mirror.h)
+        const uint32_t qb = (uint32_t)(out->quads.size() / 28), ub = (uint32_t)(out->units.size() / 16);
+        uint32_t nq = 0, nu = 0;
+        if (build_twins(out->tris.data(), nd.first_index, nd.prim_count, out->quads, out->units, &nq, &nu)) {
+            float* second = &out->tris[((size_t)nd.first_index + 1) * 12];
+            float* third = &out->tris[((size_t)nd.first_index + 2) * 12];
+            std::memcpy(&second[10], &qb, 4);
+            std::memcpy(&second[11], &nq, 4);
+            std::memcpy(&third[10], &ub, 4);
+            std::memcpy(&third[11], &nu, 4);
         }
     }
     // every root's K3.x: the leaf-tree triangle count, the stride of their field-major device copy
@@ -276,16 +382,17 @@ int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owne
     const std::vector<float> lt = rt_ltris_device_layout(m.ltris);
     // the parts in one block, each starting on a 256-B boundary (pairs of nodes and records on
     // cache-line boundaries: mirror.h)
-    const std::vector<float>* parts[8] = {&m.nodes, &m.tris, &m.pairs, &m.tree, &lt, &m.spairs, &m.flat, &m.treelets};
-    size_t off[8], total = 0;
-    for (int i = 0; i < 8; i++) {
+    const std::vector<float>* parts[10] = {&m.nodes, &m.tris, &m.pairs, &m.tree, &lt, &m.spairs, &m.flat, &m.treelets, &m.quads,
+                                           &m.units};
+    size_t off[10], total = 0;
+    for (int i = 0; i < 10; i++) {
         off[i] = total;
         total += (parts[i]->size() * 4 + 255) & ~(size_t)255;
     }
     void* block = nullptr;
     if (rt_malloc(&block, total + 256) != 0) return -1;
     char* b = static_cast<char*>(block);
-    for (int i = 0; i < 8; i++)
+    for (int i = 0; i < 10; i++)
         if (!parts[i]->empty() && rt_memcpy_h2d(b + off[i], parts[i]->data(), parts[i]->size() * 4) != 0) {
             rt_free(block);
             return -1;
@@ -300,6 +407,8 @@ int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owne
     e.dev.spairs = at(5);
     e.dev.flat = at(6);
     e.dev.treelets = at(7);
+    e.dev.quads = at(8);
+    e.dev.units = at(9);
     e.dev.depth = m.depth;
     e.dev.fast = m.fast;
     e.dev.screens = m.screens;

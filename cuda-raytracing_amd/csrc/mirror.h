@@ -15,6 +15,18 @@
 //           pf = 3 when a screen record (leaftree.h rt_build_leaf_screen: the cull record of the
 //           leaf's core and the positions of its few big "outlier" triangles) sits in the 80-B slot
 //           just before the pairs, at po - 1 (rt_fast.h screen_leaf);
+//  * quads / units  for the same leaves, their triangles by TWINS.  The reference adds every loaded
+//           face twice (Scene.cpp:103-127: the indexed face and AddTriangle's flat copy), and the two
+//           records share v0 with e1 and e2 swapped -- the same triangle, wound the other way -- so a
+//           twin's glm test computes, in real arithmetic, det' = -det, u' = -v, v' = -u.  A unit is a
+//           triangle of the leaf and its twin (if the leaf holds one), in leaf order of the first;
+//           a unit record (64 B) is the triangle record with (twin face, pos | twin pos << 16) in its
+//           last two words, then (kd, ke, 0, 0) (rt_twin_bounds; kd = -1: no twin).  A quad (112 B)
+//           packs two units for packed fp32: the pairs layout (x5), (kd_a, kd_b, ke_a, ke_b),
+//           (pos_a | twin_a << 16, pos_b | twin_b << 16, twin face a, twin face b).  A twin is tested
+//           only when its partner's own values cannot prove it rejected (rt_fast.h twin_rejected).
+//           The leaf's second / third tris record hold (first quad, quad count) / (first unit, unit
+//           count) in their last two words (0 quads: positions do not fit 16 bits, pairs only);
 //  * spairs for every leaf of at most BIG triangles, its triangles two by two in the pairs layout,
 //           the pair of triangles (i, i + 1) stored at record i (i = first, first + 2, ...; an
 //           odd leaf ends with an all-zero triangle), so a small leaf needs no index of its own;
@@ -54,6 +66,8 @@ struct MirrorHost {
     std::vector<float> nodes;     // 8 floats per private node (GPUBVHNode layout)
     std::vector<float> tris;      // 12 floats per record
     std::vector<float> pairs;     // 20 floats per pair
+    std::vector<float> quads;     // 28 floats per twin quad
+    std::vector<float> units;     // 16 floats per twin unit
     std::vector<float> spairs;    // 20 floats per triangle position (small leaves' pairs)
     std::vector<float> tree;      // 16 floats per leaf-tree node
     std::vector<float> ltris;     // 12 floats per leaf-tree triangle record
@@ -69,6 +83,11 @@ struct MirrorHost {
 void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t* face_indices, size_t index_count,
                      const GPUFace* faces, size_t face_count, const GPUVertex* vertices, size_t vertex_count,
                      MirrorHost* out);
+
+// The twin test's bounds of a triangle record (12 floats, mirror.h tris): kd bounds |det_A + det_twin|
+// (the computed values), ke x |o - v0|_1 bounds |u_A + v_twin| and |v_A + u_twin| (rt_fast.h
+// twin_rejected).
+void rt_twin_bounds(const float* rec, float* kd, float* ke);
 
 // The device copy of MirrorHost::ltris: field-major (record i: A at float4 i, B at n + i, C at
 // 2n + i), so a load instruction of a cluster's 16 lanes touches 2 cache lines instead of 6.
@@ -86,6 +105,8 @@ struct MirrorDevice {
     const void* nodes = nullptr;  // private node array (128-B aligned)
     const void* tris = nullptr;
     const void* pairs = nullptr;
+    const void* quads = nullptr;
+    const void* units = nullptr;
     const void* spairs = nullptr;
     const void* tree = nullptr;
     const void* ltris = nullptr;

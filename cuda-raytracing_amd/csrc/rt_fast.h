@@ -318,6 +318,7 @@ __device__ __forceinline__ Pair ld_pair(const float4* base, uint32_t p) {
 // perp = cross(dist, e1), v = dot(nd, perp)).
 struct PairEval {
     f2 det, u, v, uv, qx, qy, qz;  // q = perp
+    f2 dn;                         // |o - v0|_1 (computed; the twin test's bound, twin_rejected)
 };
 __device__ __forceinline__ PairEval pair_eval(f3 o, f3 nd, const Pair& P) {
     const f2 ndx = nd.x, ndy = nd.y, ndz = nd.z;
@@ -333,6 +334,7 @@ __device__ __forceinline__ PairEval pair_eval(f3 o, f3 nd, const Pair& P) {
     E.qz = dx * P.e1y - P.e1x * dy;
     E.v = (ndx * E.qx + ndy * E.qy) + ndz * E.qz;
     E.uv = E.u + E.v;
+    E.dn = f2{(fabsf(dx.x) + fabsf(dy.x)) + fabsf(dz.x), (fabsf(dx.y) + fabsf(dy.y)) + fabsf(dz.y)};
     return E;
 }
 
@@ -364,6 +366,138 @@ __device__ __forceinline__ void pair_test(const Ray& R, const Pair& P, Hit& h) {
 
 // device-library wave reduction (DPP), over the active lanes
 extern "C" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);
+
+// ---------------------------------------------------------------------------------------
+// Twins (mirror.h quads / units).  Every loaded face is in the scene twice (Scene.cpp:103-127), and a
+// big leaf holds both records: A = (v0, e1, e2) and its twin A' = (v0, e2, e1), so the sequential loop
+// (main_raytracing.cu:51-71) runs glm's test on each triangle twice, wound both ways.  In real
+// arithmetic the twin's det, u, v are -det, -v, -u of A's, and the fp32 values stay within bounds the
+// mirror precomputes (mirror.cpp rt_twin_bounds): |det + det'| <= kd, |u + v'|, |v + u'| <= ke |o - v0|_1.
+// So A's own values decide the twin whenever they reject it with margin; only the rest (a ray within
+// a few ulps of an edge, or nearly parallel to the plane, or a hit) test the twin itself.  Quads pack
+// two triangles (packed fp32, as the pairs) and their twins for the shared-leaf loop, units one
+// triangle and its twin for the cooperative rounds, so a leaf costs about half its records.
+// Triangles are then visited out of leaf order, so a candidate is kept by the sequential loop's own
+// rule restated in (t, position) order: below the entry distance, the smallest t, the lowest position
+// among equal t (a NaN distance: the leaf is redone sequentially).
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t NO_POS = 0xffffffffu;
+
+// Whether glm's test certainly rejects the twin of a triangle whose own test computed (det, u, v, uv)
+// at |o - v0|_1 = dn.  With the twin's det' within kd of -det, u' within m of -v and v' within m of -u
+// (m = ke dn), the twin's sign-folded quantities (test_triangle) are su' = sv +- m, sv' = su +- m,
+// suv' = suv (1 +- 2.0001 U) +- 2.0001 m and |det'| = |det| +- kd once |det| > kd fixes det's sign; it
+// fails `|det'| > eps && 0 <= su' <= |det'| && 0 <= sv' && suv' <= |det'|` if any bound already does.
+// Every threshold is widened by 2^-20 (> the rounding of these few operations) and by 2^-90 (underflow);
+// NaN, infinities and huge values are never decided here.
+RT_HD bool twin_rejected(float det, float u, float v, float uv, float dn, float kd, float ke) {
+    const bool neg = signbit(det);  // the sign fold of test_triangle (negation is exact)
+    const float ad = fabsf(det);
+    const float su = neg ? -u : u, sv = neg ? -v : v, suv = neg ? -uv : uv;
+    if (!(ad + fabsf(su) + fabsf(sv) + dn < 0x1p100f)) return false;
+    const float m = ke * dn + 0x1p-90f;
+    const float kdd = kd + 0x1p-90f;
+    const float top = (ad + kdd) * (1.0f + 0x1p-20f);
+    if (top <= 1.1920928955078125e-07f) return true;  // |det'| <= eps
+    if (!(ad > kdd * (1.0f + 0x1p-20f))) return false;  // det' may have either sign
+    if (sv < -m || su < -m) return true;                // su' < 0 or sv' < 0
+    if (sv > (ad + kdd + m) * (1.0f + 0x1p-20f)) return true;  // su' > |det'|
+    return suv * (1.0f - 0x1p-20f) > (ad + kdd + 2.001f * m) * (1.0f + 0x1p-20f);  // suv' > |det'|
+}
+
+// A candidate under the sequential loop's rule in (t, position) order (h.best is the entry distance
+// while bpos == NO_POS).
+__device__ __forceinline__ void offer(float t, uint32_t pos, uint32_t id, float bx, float by, Hit& h, uint32_t& bpos,
+                                      bool& nan) {
+    if (t != t) {
+        nan = true;
+        return;
+    }
+    if (t >= 0.0f && (t < h.best || (t == h.best && bpos != NO_POS && pos < bpos)))
+        h.best = t, h.kind = 2, h.id = id, h.bx = bx, h.by = by, bpos = pos;
+}
+
+// glm's test of triangle (v0, e1, e2) (test_triangle's operation order) offered at `pos`.
+__device__ __forceinline__ void tri_offer(f3 o, f3 nd, f3 v0, f3 e1, f3 e2, uint32_t pos, uint32_t face, Hit& h,
+                                          uint32_t& bpos, bool& nan) {
+    const f3 p = rtm::cross(nd, e2);
+    const float det = rtm::dot(e1, p);
+    const f3 dist = rtm::sub(o, v0);
+    const float u = rtm::dot(dist, p);
+    const f3 perp = rtm::cross(dist, e1);
+    const float v = rtm::dot(nd, perp);
+    if (tri_ok(det, u, v, u + v)) {
+        const float inv_det = 1.0f / det;
+        offer(rtm::dot(e2, perp) * inv_det, pos, face, u * inv_det, v * inv_det, h, bpos, nan);
+    }
+}
+
+// Quads (mirror.h): 7 float4 -- the pair layout (x5), the twin bounds (kd_a, kd_b, ke_a, ke_b; kd < 0:
+// no twin), and (pos_a | twin_a << 16, pos_b | twin_b << 16, twin face a, twin face b), read only on a
+// hit or a twin test.  One quad for one ray (the shared-leaf loop: scalar loads).
+__device__ __forceinline__ void quad_test(f3 o, f3 nd, const Pair& P, f4v bnd, ConstF4 q6, Hit& h, uint32_t& bpos,
+                                          bool& nan) {
+    const PairEval E = pair_eval(o, nd, P);
+    const bool oka = tri_ok(E.det.x, E.u.x, E.v.x, E.uv.x), okb = tri_ok(E.det.y, E.u.y, E.v.y, E.uv.y);
+    const bool twa = bnd.x >= 0.0f && !twin_rejected(E.det.x, E.u.x, E.v.x, E.uv.x, E.dn.x, bnd.x, bnd.z);
+    const bool twb = bnd.y >= 0.0f && !twin_rejected(E.det.y, E.u.y, E.v.y, E.uv.y, E.dn.y, bnd.y, bnd.w);
+    if (oka || okb || twa || twb) {  // rare: a hit, or a twin too close to call
+        const f4v W = *q6;
+        const uint32_t wa = __float_as_uint(W.x), wb = __float_as_uint(W.y);
+        if (oka) {
+            float inv;
+            const float t = pair_t(P, E, 0, &inv);
+            offer(t, wa & 0xffffu, P.fa, E.u.x * inv, E.v.x * inv, h, bpos, nan);
+        }
+        if (okb) {
+            float inv;
+            const float t = pair_t(P, E, 1, &inv);
+            offer(t, wb & 0xffffu, P.fb, E.u.y * inv, E.v.y * inv, h, bpos, nan);
+        }
+        if (twa)
+            tri_offer(o, nd, rtm::mk(P.v0x.x, P.v0y.x, P.v0z.x), rtm::mk(P.e2x.x, P.e2y.x, P.e2z.x),
+                      rtm::mk(P.e1x.x, P.e1y.x, P.e1z.x), wa >> 16, __float_as_uint(W.z), h, bpos, nan);
+        if (twb)
+            tri_offer(o, nd, rtm::mk(P.v0x.y, P.v0y.y, P.v0z.y), rtm::mk(P.e2x.y, P.e2y.y, P.e2z.y),
+                      rtm::mk(P.e1x.y, P.e1y.y, P.e1z.y), wb >> 16, __float_as_uint(W.w), h, bpos, nan);
+    }
+}
+
+// Units (mirror.h): 4 float4 -- a triangle record (v0, e1, e2, face) with (twin face, pos | twin << 16)
+// in its last two words, and (kd, ke, 0, 0); kd < 0: no twin.  One unit for one ray (cooperative
+// rounds: a lane per unit).
+__device__ __forceinline__ void unit_test(f3 o, f3 nd, float4 A, float4 B, float4 Cc, float4 D, Hit& h, uint32_t& bpos,
+                                          bool& nan) {
+    const f3 v0 = rtm::mk(A.x, A.y, A.z), e1 = rtm::mk(A.w, B.x, B.y), e2 = rtm::mk(B.z, B.w, Cc.x);
+    const f3 p = rtm::cross(nd, e2);
+    const float det = rtm::dot(e1, p);
+    const f3 dist = rtm::sub(o, v0);
+    const float u = rtm::dot(dist, p);
+    const f3 perp = rtm::cross(dist, e1);
+    const float v = rtm::dot(nd, perp);
+    const float uv = u + v;
+    const uint32_t w = __float_as_uint(Cc.w);
+    if (tri_ok(det, u, v, uv)) {
+        const float inv_det = 1.0f / det;
+        offer(rtm::dot(e2, perp) * inv_det, w & 0xffffu, __float_as_uint(Cc.y), u * inv_det, v * inv_det, h, bpos, nan);
+    }
+    const float dn = (fabsf(dist.x) + fabsf(dist.y)) + fabsf(dist.z);
+    if (D.x >= 0.0f && !twin_rejected(det, u, v, uv, dn, D.x, D.y))
+        tri_offer(o, nd, v0, e2, e1, w >> 16, __float_as_uint(Cc.z), h, bpos, nan);
+}
+
+// BVHRayHit's sequential loop over big leaf [f0, f0 + c0) for this lane (the NaN fallback).
+__device__ __forceinline__ void leaf_sequential(const float4* tris, uint32_t f0, uint32_t c0, f3 o, f3 nd, Hit& h) {
+    for (uint32_t j = 0; j < c0; j++) {
+        const float4 A = tris[3 * (f0 + j)], B = tris[3 * (f0 + j) + 1], Cc = tris[3 * (f0 + j) + 2];
+        float t, x, y;
+        bool dummy = false;
+        if (tri_accept(o, nd, A, B, Cc, h.best, &t, &x, &y, &dummy)) {
+            h.best = t, h.kind = 2, h.bx = x, h.by = y;
+            h.id = __float_as_uint(Cc.y);
+        }
+    }
+}
 
 // Order-preserving key of a distance t >= 0 (found candidates only): +-0 share key 0, so a tie
 // between them is decided by position, as the float comparison `t == best` does.
@@ -431,6 +565,40 @@ __device__ __forceinline__ void coop_leaf(const float4* tris, const float4* pair
             const int wl = (int)((mi >> 1) & 63u);  // lane that tested pair mi / 2
             const float wbx = bcast(bx, wl), wby = bcast(by, wl), wt = bcast(bt, wl);
             const uint32_t wid = (uint32_t)__builtin_amdgcn_readlane((int)bid, wl);
+            if ((int)lane == r) h.best = wt, h.kind = 2, h.bx = wbx, h.by = wby, h.id = wid;
+        }
+    }
+}
+
+// coop_leaf on a leaf's units (mirror.h): lane l tests units l, l + 64, ... for the one ray, keeping
+// its (t, position)-first candidate (offer); the wave's (t, position) arg-min is the sequential loop's
+// result.  A NaN distance, or a NaN entry distance, runs the sequential loop.
+__device__ __forceinline__ void coop_units(const float4* tris, const float4* un, uint32_t nu, unsigned long long big,
+                                           uint32_t f0, uint32_t c0, const Ray& R, Hit& h) {
+    const uint32_t lane = threadIdx.x & 63u;
+    unsigned long long m = big;
+    while (m) {
+        const int r = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const f3 rox = rtm::mk(bcast(R.o.x, r), bcast(R.o.y, r), bcast(R.o.z, r));
+        const f3 nd = rtm::mk(bcast(R.nd.x, r), bcast(R.nd.y, r), bcast(R.nd.z, r));
+        Hit L;
+        L.best = bcast(h.best, r), L.kind = 0, L.id = 0, L.bx = L.by = 0.0f;
+        uint32_t bpos = NO_POS;
+        bool nan = !(L.best == L.best);
+        for (uint32_t q = lane; q < nu; q += 64u)
+            unit_test(rox, nd, un[4 * q], un[4 * q + 1], un[4 * q + 2], un[4 * q + 3], L, bpos, nan);
+        if (__ballot(nan)) {
+            if ((int)lane == r) leaf_sequential(tris, f0, c0, R.o, R.nd, h);
+            continue;
+        }
+        const bool has = bpos != NO_POS;
+        const uint32_t mk = __ockl_wfred_min_u32(has ? tkey(L.best) : 0xffffffffu);
+        const uint32_t mi = __ockl_wfred_min_u32(has && tkey(L.best) == mk ? bpos : 0xffffffffu);
+        if (mi != 0xffffffffu) {
+            const int wl = __ffsll((long long)__ballot(has && bpos == mi)) - 1;
+            const float wt = bcast(L.best, wl), wbx = bcast(L.bx, wl), wby = bcast(L.by, wl);
+            const uint32_t wid = (uint32_t)__builtin_amdgcn_readlane((int)L.id, wl);
             if ((int)lane == r) h.best = wt, h.kind = 2, h.bx = wbx, h.by = wby, h.id = wid;
         }
     }
@@ -881,7 +1049,8 @@ __device__ __forceinline__ bool small_step(const float4* nodes4, const float4* t
 // lane is at that leaf, or each lane alone otherwise (MODE: see trace).  Returns whether this
 // lane ran its leaf (it then pops; the others keep waiting).
 template <bool STATS, int MODE, class C>
-__device__ __forceinline__ bool big_round(const float4* tris, const float4* pairs, const float4* tree,
+__device__ __forceinline__ bool big_round(const float4* tris, const float4* pairs, const float4* quads, const float4* units,
+                                          const float4* tree,
                                           const float4* ltris, const float4* flat, uint32_t* scratch, uint32_t tune,
                                           unsigned long long big, bool waiting,
                                           const Ray& R, Hit& h, const Trav& T, C& c) {
@@ -917,9 +1086,39 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
         c.l_big += waiting ? T.count : 0;
     }
     if (__ballot(waiting && T.first == f0) == big) {
-        // the first record of a big leaf says where its pairs are (mirror.h)
+        // the first record of a big leaf says where its pairs are, the second where its twin quads are (mirror.h)
         const f4v lead = ((ConstF4)(tris + 3 * (size_t)f0))[2];
         const uint32_t k = (uint32_t)__popcll(big);
+        if (!STATS && (MODE & 3) < 2 && quads && (__float_as_uint(lead.w) & 1u)) {
+            // the second record: the leaf's first quad and quad count, the third: first unit and count
+            const f4v l2 = ((ConstF4)(tris + 3 * (size_t)f0 + 3))[2];
+            const f4v l3 = ((ConstF4)(tris + 3 * (size_t)f0 + 6))[2];
+            const uint32_t nq = __float_as_uint(l2.w), nu = __float_as_uint(l3.w);
+            // cost model (VALU instructions): cooperative ~ k * (70 * chunks + 70) over the units,
+            // shared ~ 95 * nq over the quads for all waiting lanes at once
+            if (nu && (tune & 1u) == 0 && k * (70u * ((nu + 63u) / 64u) + 70u) < 95u * nq) {
+                coop_units(tris, units + 4 * (size_t)__float_as_uint(l3.z), nu, big, f0, c0, R, h);
+                if (MODE & 8) c.r_coop++, c.coop_rays += k;
+                return waiting;
+            }
+            if (nq) {
+                if (MODE & 8) c.r_shared++;
+                const Hit h0 = h;
+                uint32_t bpos = NO_POS;
+                bool nan = !(h.best == h.best);
+                ConstF4 qs = (ConstF4)(quads + 7 * (size_t)__float_as_uint(l2.z));
+                for (uint32_t q = 0; q < nq; q++, qs += 7) {
+                    const Pair P = make_pair(qs[0], qs[1], qs[2], qs[3], qs[4]);
+                    const f4v bnd = qs[5];
+                    if (waiting) quad_test(R.o, R.nd, P, bnd, qs + 6, h, bpos, nan);
+                }
+                if (waiting && nan) {  // the sequential loop from the entry distance (never taken for finite scenes)
+                    h = h0;
+                    leaf_sequential(tris, f0, c0, R.o, R.nd, h);
+                }
+                return waiting;
+            }
+        }
         if (!STATS && (MODE & 3) < 2 && pairs && (__float_as_uint(lead.w) & 1u)) {
             const float4* lp = pairs + 5 * (size_t)__float_as_uint(lead.z);
             const uint32_t np = (c0 + 1u) / 2u, chunks = (np + 63u) / 64u;
@@ -1148,7 +1347,8 @@ template <bool STATS, int MODE, class S, class C>
 __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, const float4* pairs,
                                       const float4* tree, const float4* ltris, const float4* flat,
                                       const float4* spairs, uint32_t tune, const S& stk, uint32_t* scratch,
-                                      const Ray& R, Hit& h, bool live, C& c) {
+                                      const Ray& R, Hit& h, bool live, C& c, const float4* quads = nullptr,
+                                      const float4* units = nullptr) {
     Trav T{0, 0, 0};
     bool active = live && trav_begin<STATS>(nodes4, R, h, T, c);
     // big-leaf screens (screen_leaf, MODE bit 5): split-step variants for scenes that have them
@@ -1246,7 +1446,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
         }
         const unsigned long long big = __ballot(active);  // every active lane waits at a big leaf
         if (!big) break;
-        if (big_round<STATS, MODE>(tris, pairs, tree, ltris, flat, scratch, tune, big, active, R, h, T, c)) {
+        if (big_round<STATS, MODE>(tris, pairs, quads, units, tree, ltris, flat, scratch, tune, big, active, R, h, T, c)) {
             // a big leaf run alone (cooperative round) costs about as much as 3 small steps
             if (TIMING) c.lane_work += 3;
             if constexpr (scr_on) T.sp &= ~SCREENED;

@@ -15,14 +15,13 @@ hipError_t dispatch(int mode, const RenderArgs& a, int waves, hipStream_t s) {
 }  // namespace
 
 hipError_t launch_fast_ab2(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);
+hipError_t launch_fast_ab1(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);
+RT_FAST_FAMILY(launch_fast_ab1, dispatch)
 
-namespace {
-hipError_t ab1(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);
-RT_FAST_FAMILY(ab1, dispatch)
-}  // namespace
-
+#if !defined(RT_W6_ONLY)
 hipError_t launch_fast_ab(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s) {
-    return (mode == 2 || mode == 0) ? launch_fast_ab2(stack, mode, a, waves, s) : ab1(stack, mode, a, waves, s);
+    return (mode == 2 || mode == 0) ? launch_fast_ab2(stack, mode, a, waves, s) : launch_fast_ab1(stack, mode, a, waves, s);
 }
+#endif
 
 }  // namespace rtk

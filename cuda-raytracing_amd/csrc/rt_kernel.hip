@@ -457,7 +457,8 @@ void upload_mirror(ForeignBuild* b) {
         rt_build_mirror(nodes, b->bytes[0] / sizeof(GPUBVHNode), fi, b->bytes[1] / 4, faces, b->bytes[2] / sizeof(GPUFace),
                         verts, b->bytes[3] / sizeof(GPUVertex), &mh);
         const std::vector<float> lt = rt_ltris_device_layout(mh.ltris);
-        const std::vector<float>* parts[8] = {&mh.tris, &mh.pairs, &mh.tree, &lt, &mh.spairs, &mh.flat, &mh.treelets, &mh.nodes};
+        const std::vector<float>* parts[10] = {&mh.tris, &mh.pairs, &mh.tree, &lt, &mh.spairs, &mh.flat, &mh.treelets, &mh.nodes,
+                                               &mh.quads, &mh.units};
         size_t total = 256;  // each part on a 256-B boundary (mirror.h: cache-line aligned pairs)
         for (auto* v : parts) total += (v->size() * 4 + 255) & ~(size_t)255;
         hipStream_t st;
@@ -465,8 +466,8 @@ void upload_mirror(ForeignBuild* b) {
         void* block = nullptr;
         if (hipMallocAsync(&block, total, st) != hipSuccess) throw std::runtime_error("mirror allocation failed");
         char* p = static_cast<char*>(block);
-        const void* where[8];
-        for (int i = 0; i < 8; i++) {
+        const void* where[10];
+        for (int i = 0; i < 10; i++) {
             const size_t nb = parts[i]->size() * 4;
             where[i] = nb ? p : nullptr;
             if (nb && hipMemcpyAsync(p, parts[i]->data(), nb, hipMemcpyHostToDevice, st) != hipSuccess)
@@ -479,6 +480,7 @@ void upload_mirror(ForeignBuild* b) {
         b->block = block;
         b->dev.tris = where[0], b->dev.pairs = where[1], b->dev.tree = where[2], b->dev.ltris = where[3];
         b->dev.spairs = where[4], b->dev.flat = where[5], b->dev.treelets = where[6], b->dev.nodes = where[7];
+        b->dev.quads = where[8], b->dev.units = where[9];
         b->dev.depth = mh.depth, b->dev.fast = mh.fast, b->dev.owned = false, b->dev.fingerprint = b->fingerprint;
         b->dev.screens = mh.screens;
         b->state = 2;
@@ -776,6 +778,8 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     const bool scene_fast = mir.fast;
     a.tune = p->tune;  // diagnostic A/B knobs; 0 = the production path
     a.pairs = (a.tune & 2u) ? nullptr : (const float4*)mir.pairs;
+    a.quads = (a.tune & ((1u << 20) | 2u)) ? nullptr : (const float4*)mir.quads;  // RT_TUNE bit 20: no twins
+    a.units = (const float4*)mir.units;
     a.tree = (a.tune & 4u) ? nullptr : (const float4*)mir.tree;
     a.ltris = (const float4*)mir.ltris;
     a.spairs = (a.tune & 8u) ? nullptr : (const float4*)mir.spairs;
@@ -967,6 +971,36 @@ extern "C" void init_rng(uint32_t thread_block_count, uint32_t thread_block_size
 
 // Diagnostics: the leaf-tree cull predicate of the render kernel, evaluated on the host by the
 // same code (tests/test_leaf_tree.py).
+// The twin test (rt_fast.h twin_rejected) on the host, for tests/test_scene.py: triangle record `rec`
+// (mirror.h tris) and its twin (v0, e2, e1) under glm's test (test_triangle's operation order) for the
+// ray (o, nd); bit 0: twin_rejected, bit 1: the twin passes glm's predicate, bit 2: A passes it.
+extern "C" int rt_twin_check_host(const float rec[12], const float o[3], const float nd[3]) {
+    using rtm::f3;
+    const f3 O = rtm::mk(o[0], o[1], o[2]), N = rtm::mk(nd[0], nd[1], nd[2]), v0 = rtm::mk(rec[0], rec[1], rec[2]);
+    const f3 e1 = rtm::mk(rec[3], rec[4], rec[5]), e2 = rtm::mk(rec[6], rec[7], rec[8]);
+    auto glm = [&](f3 a, f3 b, float* det, float* u, float* v, float* uv) {  // (e1, e2) = (a, b)
+        const f3 p = rtm::cross(N, b);
+        *det = rtm::dot(a, p);
+        const f3 dist = rtm::sub(O, v0);
+        *u = rtm::dot(dist, p);
+        *v = rtm::dot(N, rtm::cross(dist, a));
+        *uv = *u + *v;
+    };
+    auto ok = [](float det, float u, float v, float uv) {
+        const bool neg = signbit(det);
+        const float ad = fabsf(det), su = neg ? -u : u, sv = neg ? -v : v, suv = neg ? -uv : uv;
+        return ad > 1.1920928955078125e-07f && !(su < 0.0f || su > ad) && !(sv < 0.0f || suv > ad);
+    };
+    float d, u, v, uv, d2, u2, v2, uv2;
+    glm(e1, e2, &d, &u, &v, &uv);
+    glm(e2, e1, &d2, &u2, &v2, &uv2);
+    const f3 dist = rtm::sub(O, v0);
+    const float dn = (fabsf(dist.x) + fabsf(dist.y)) + fabsf(dist.z);
+    float kd, ke;
+    rt_twin_bounds(rec, &kd, &ke);
+    return (rtfast::twin_rejected(d, u, v, uv, dn, kd, ke) ? 1 : 0) | (ok(d2, u2, v2, uv2) ? 2 : 0) | (ok(d, u, v, uv) ? 4 : 0);
+}
+
 extern "C" int rt_cluster_cull_host(const float origin[3], const float nd[3], float best, const float node[16]) {
     rtfast::Ray R;
     R.o = rtm::mk(origin[0], origin[1], origin[2]);

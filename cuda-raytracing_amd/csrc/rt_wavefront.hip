@@ -328,7 +328,7 @@ __device__ __forceinline__ void wf_trace_body(const RenderArgs& a, const WfBuf& 
             continue;
         }
         if (!mW) continue;
-        if (rtfast::big_round<false, MODE>(tris, a.pairs, a.tree, a.ltris, a.flat, scratch_lds, a.tune, mW, waiting, R, h,
+        if (rtfast::big_round<false, MODE>(tris, a.pairs, a.quads, a.units, a.tree, a.ltris, a.flat, scratch_lds, a.tune, mW, waiting, R, h,
                                            T, c))
             active = rtfast::pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
     }

@@ -479,6 +479,10 @@ int rt_bvh_build_device(const GPUVertex* vertices, uint32_t vertex_count, const 
 int rt_scene_mirror_info(rt_scene* scene, size_t* tri_records, size_t* tree_nodes, size_t* tree_tri_records);
 int rt_scene_mirror_copy(rt_scene* scene, float* tris, float* tree, float* tree_tris);
 int rt_cluster_cull_host(const float origin[3], const float nd[3], float best, const float node[16]);
+/* The twin test of the big-leaf quads (rt_fast.h twin_rejected, mirror.h quads) on the host: bit 0
+   the twin of triangle record `rec` (v0, e2, e1) is proven rejected from rec's own glm values for the
+   ray (origin, nd), bit 1 the twin passes glm's predicate, bit 2 rec does.  For tests. */
+int rt_twin_check_host(const float rec[12], const float origin[3], const float nd[3]);
 /* The traversal's private node array (mirror.h nodes: GPUBVHNode records, sibling pairs 64-B
    aligned in right-first pre-order), built on the host: *count receives the node count; nodes (may
    be NULL) receives the records.  0 or -1 with rt_last_error(). */

@@ -200,3 +200,37 @@ def test_config3_sharded_8way_equals_unsharded(rt):
     ref, rng_ref = render_gpu(rt, "bunny", w, h, spp, b, tracer="ref")
     report("config3 full frame: production vs reference-layout tracer, 3840x2160 64spp", full, ref)
     assert np.array_equal(rng_full, rng_ref)
+
+
+_ORACLE_SMALL = {}
+
+
+@pytest.mark.parametrize("which,screens", [("bunny", 0), ("bunny4", 0), ("bunny4", 1), ("plane1m", 0)])
+@pytest.mark.parametrize("wps", [5, 6, 7])
+def test_every_occupancy_build_equals_oracle(rt, which, screens, wps):
+    """Every occupancy build of the production kernel (5 / 6 / 7 waves per SIMD, the ones bench.py's
+    probe chooses among) against the oracle, including the mirror with big-leaf screen records: the
+    6-wave leaf-tree kernel built with -structurizecfg-skip-uniform-regions once rendered 2,196 of
+    36,864 pixels of this 4-bunny frame wrong (build.py W6_SPLIT)."""
+    w, h, spp, bounces = 256, 144, 2, 6
+    key = (which, w, h, spp)
+    if key not in _ORACLE_SMALL:
+        _ORACLE_SMALL[key] = T.OracleScene(which).render(w, h, spp, bounces, threads=threads())
+    want = _ORACLE_SMALL[key]
+    if screens:
+        rt.set_build_options(leaf_screens=1)
+    try:
+        s = rt.Scene()
+        s.setup(which)
+        s.set_viewport(w, h)
+        rng = rt.alloc_rng(w * h)
+        rt.init_rng_states(rng, w, h, T.SEED)
+        s.upload(rng.data_ptr())
+        a, b = rt.alloc_surface(w, h), rt.alloc_surface(w, h)
+        rt.render(s, a, b, w, h, spp, bounces, waves_per_simd=wps, tune=(1 << 28) if screens else 0)
+        torch.cuda.synchronize()
+        got = rt.surface_view(a, w).cpu().numpy()
+    finally:
+        rt.set_build_options()
+    bad = int((got.view(np.uint32) != want.view(np.uint32)).any(-1).sum())
+    assert bad == 0, f"{which} screens={screens} at {wps} waves per SIMD: {bad} pixels differ from the oracle"

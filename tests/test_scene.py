@@ -162,3 +162,62 @@ def _big_leaf_flags(rt, which):
         nodes = s.host_arrays()["nodes"].view(np.uint32).reshape(-1, 8)
         big = nodes[(nodes[:, 7] > 8)]
         return {int(n[7]): int(tris[n[6], 11]) for n in big}
+
+
+@pytest.mark.parametrize("which", ["bunny", "bunny4"])
+def test_twin_quads_and_bound(which):
+    """mirror.h quads: every big leaf (pair records) lists each of its triangles exactly once, as a
+    quad member or as the twin (same v0, e1 and e2 swapped, bit for bit) of one -- nearly all of them
+    are twins, the reference adds every loaded face twice (Scene.cpp:103-127).  And the twin test
+    (rt_fast.h twin_rejected, run here on the host by the same code): over rays aimed at the edges and
+    vertices, grazing the plane and random, a twin it declares rejected never passes glm's predicate,
+    while it does decide most rays."""
+    import ctypes
+    rt = T.load_rt()
+    s = rt.Scene()
+    s.setup(which)
+    s.build()
+    tris = s.mirror()
+    tu = tris.view(np.uint32).reshape(-1, 12)
+    leads = [i for i in range(tu.shape[0]) if tu[i, 11] in (1, 3)]
+    assert leads
+    nodes = s.host_arrays()["nodes"].view(np.uint32).reshape(-1, 8)
+    counts = {int(n[6]): int(n[7]) for n in nodes if n[7] > 0}
+    twins = 0
+    for f in leads:
+        c = counts[f]
+        nq = int(tu[f + 1, 11])
+        keys = {}
+        for i in range(c):
+            r = tu[f + i]
+            keys.setdefault((r[:3].tobytes(), r[3:6].tobytes(), r[6:9].tobytes()), []).append(i)
+        tw = sum(1 for i in range(c) if (tu[f + i, :3].tobytes(), tu[f + i, 6:9].tobytes(), tu[f + i, 3:6].tobytes()) in keys)
+        twins += tw
+        assert (c + 3) // 4 <= nq <= (c + 1) // 2, "two units (a triangle and its twin, or a lone triangle) per quad"
+    assert twins > 0.9 * sum(counts[f] for f in leads), "big leaves are twins (Scene.cpp:103-127)"
+    lib = rt.lib()
+    gen = np.random.default_rng(7)
+    f = max(leads, key=lambda x: counts[x])
+    rec = tris[f:f + counts[f]]
+    bad = decided = total = 0
+    for k in range(min(counts[f], 120)):
+        r = np.ascontiguousarray(rec[k], dtype=np.float32)
+        v0, e1, e2 = r[:3], r[3:6], r[6:9]
+        pts = [v0, v0 + e1, v0 + e2, v0 + 0.5 * e1, v0 + 0.5 * e2, v0 + 0.5 * (e1 + e2)]
+        nrm = np.cross(e1.astype(np.float64), e2.astype(np.float64))
+        nrm /= np.linalg.norm(nrm) + 1e-300
+        for trial in range(60):
+            target = pts[trial % len(pts)] + gen.normal(size=3) * 10.0 ** gen.uniform(-7, -1) * np.abs(e1).max()
+            o = (target + gen.normal(size=3) * 10.0 ** gen.uniform(-1, 2)).astype(np.float32)
+            d = (target - o).astype(np.float64)
+            if trial % 3 == 1:  # grazing: nearly in the triangle's plane
+                d -= nrm * (d @ nrm) * (1 - 10.0 ** gen.uniform(-7, -1))
+            if trial % 5 == 4:
+                d = gen.normal(size=3)
+            nd = (d / np.linalg.norm(d)).astype(np.float32)
+            b = lib.rt_twin_check_host(r.ctypes.data, o.ctypes.data, nd.ctypes.data)
+            total += 1
+            decided += b & 1
+            bad += (b & 1) and (b & 2)
+    assert bad == 0, f"{bad} twins declared rejected but accepted by glm's predicate"
+    assert decided > 0.5 * total, (decided, total)

@@ -1,6 +1,6 @@
 """Phase clocks of one frame (timing variant of the production kernel, RT_TUNE bit 8): wave cycles
 in small steps (inner nodes / small leaves), big-leaf rounds, and the rest (shading, sky, RNG,
-output), summed over waves.  python tools/phase_clocks.py [cfg2]"""
+output), summed over waves.  python tools/phase_clocks.py [cfg2] [waves per SIMD]"""
 import json
 import os
 import sys
@@ -26,11 +26,13 @@ rt.init_rng_states(rng, W, H, bench.SEED)
 scene.upload(rng.data_ptr())
 a, b = rt.alloc_surface(W, H), rt.alloc_surface(W, H)
 st = torch.zeros(24, dtype=torch.int64, device="cuda")
-rt.render(scene, a, b, W, H, SPP, BOUNCES, 0, stats=st, tune=256)
+wps = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+rt.render(scene, a, b, W, H, SPP, BOUNCES, 0, stats=st, tune=256 | ({6: 2, 7: 3}.get(wps, 0) << 9))
 torch.cuda.synchronize()
 v = st.cpu().numpy()
 small, big, total = int(v[16]), int(v[17]), int(v[18])
-print(json.dumps({"config": sys.argv[1] if len(sys.argv) > 1 else "cfg2", "wave_cycles_total": total,
+print(json.dumps({"config": sys.argv[1] if len(sys.argv) > 1 else "cfg2", "waves_per_simd": wps or 5,
+                  "wave_cycles_total": total,
                   "small_frac": round(small / total, 3), "big_frac": round(big / total, 3),
                   "rest_frac": round(1 - (small + big) / total, 3), "rounds_coop": int(v[19]), "rounds_shared": int(v[20]),
                   "coop_rays": int(v[21]), "wave_small_iters": int(v[8]), "lane_small": int(v[9]),
