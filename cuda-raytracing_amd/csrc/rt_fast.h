@@ -69,9 +69,17 @@ __device__ __forceinline__ void slab_exact(const Ray& R, float4 lo, float4 hi, f
 // Approximate slab: same numerators (b - o, exact as in the reference), quotients by
 // multiplication with RN(1/d).  Only called when R.fast (no NaN / inf / subnormal).
 __device__ __forceinline__ void slab_approx(const Ray& R, float4 lo, float4 hi, float* tmin_o, float* tmax_o) {
+#ifdef RT_PK_SLAB  // A/B (tools/build_variant.sh): the six subtractions / products as packed pairs
+    typedef float p2 __attribute__((ext_vector_type(2)));
+    const p2 ta = (p2{lo.x, lo.y} - p2{R.o.x, R.o.y}) * p2{R.r.x, R.r.y};
+    const p2 tb = (p2{lo.z, lo.w} - p2{R.o.z, R.o.x}) * p2{R.r.z, R.r.x};
+    const p2 tc = (p2{hi.x, hi.y} - p2{R.o.y, R.o.z}) * p2{R.r.y, R.r.z};
+    const float tx1 = ta.x, ty1 = ta.y, tz1 = tb.x, tx2 = tb.y, ty2 = tc.x, tz2 = tc.y;
+#else
     const float tx1 = (lo.x - R.o.x) * R.r.x, tx2 = (lo.w - R.o.x) * R.r.x;
     const float ty1 = (lo.y - R.o.y) * R.r.y, ty2 = (hi.x - R.o.y) * R.r.y;
     const float tz1 = (lo.z - R.o.z) * R.r.z, tz2 = (hi.y - R.o.z) * R.r.z;
+#endif
     *tmin_o = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
     *tmax_o = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
 }
@@ -1096,7 +1104,9 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
             const uint32_t nq = __float_as_uint(l2.w), nu = __float_as_uint(l3.w);
             // cost model (VALU instructions): cooperative ~ k * (70 * chunks + 70) over the units,
             // shared ~ 95 * nq over the quads for all waiting lanes at once
-            if (nu && (tune & 1u) == 0 && k * (70u * ((nu + 63u) / 64u) + 70u) < 95u * nq) {
+            // RT_TUNE bits 21-23: the cooperative side's weight in quarters (0 = 4, the default)
+            const uint32_t cw = (tune >> 21) & 7u;
+            if (nu && (tune & 1u) == 0 && k * (70u * ((nu + 63u) / 64u) + 70u) * (cw ? cw : 4u) < 4u * 95u * nq) {
                 coop_units(tris, units + 4 * (size_t)__float_as_uint(l3.z), nu, big, f0, c0, R, h);
                 if (MODE & 8) c.r_coop++, c.coop_rays += k;
                 return waiting;
