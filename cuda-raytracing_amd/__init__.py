@@ -155,6 +155,7 @@ SIGNATURES = {
     "rt_scene_mirror_info": (_I, [_P, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
     "rt_scene_mirror_copy": (_I, [_P, _P, _P, _P]),
     "rt_scene_mirror_nodes": (_I, [_P, _P, ctypes.POINTER(_SZ)]),
+    "rt_scene_mirror_twins": (_I, [_P, _P, ctypes.POINTER(_SZ), _P, ctypes.POINTER(_SZ)]),
     "rt_cluster_cull_host": (_I, [_P, _P, ctypes.c_float, _P]),
     "rt_twin_check_host": (_I, [_P, _P, _P]),
     "rt_xorwow_jump_matrix": (_I, [_I, ctypes.POINTER(ctypes.c_uint32)]),
@@ -321,6 +322,17 @@ class Scene:
         out = np.zeros((n.value, 8), dtype=np.float32)
         _check(lib().rt_scene_mirror_nodes(self.handle, out.ctypes.data, ctypes.byref(n)), "rt_scene_mirror_nodes")
         return out
+
+    def mirror_twins(self):
+        """The big leaves' twin records (mirror.h): quads (Q, 28) and units (U, 16) float32."""
+        import numpy as np
+        nq, nu = ctypes.c_size_t(), ctypes.c_size_t()
+        _check(lib().rt_scene_mirror_twins(self.handle, None, ctypes.byref(nq), None, ctypes.byref(nu)), "rt_scene_mirror_twins")
+        q = np.zeros((nq.value, 28), dtype=np.float32)
+        u = np.zeros((nu.value, 16), dtype=np.float32)
+        _check(lib().rt_scene_mirror_twins(self.handle, q.ctypes.data, ctypes.byref(nq), u.ctypes.data, ctypes.byref(nu)),
+               "rt_scene_mirror_twins")
+        return q, u
 
     def host_arrays(self):
         """numpy copies of the host arrays: nodes (N,8) f32/u32 view, face indices, vertices, faces."""

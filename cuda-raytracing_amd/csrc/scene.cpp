@@ -715,6 +715,15 @@ int rt_scene_mirror_nodes(rt_scene* s, GPUBVHNode* nodes, size_t* count) {
     if (nodes) std::memcpy(nodes, m.nodes.data(), m.nodes.size() * 4);
     return 0;
 }
+int rt_scene_mirror_twins(rt_scene* s, float* quads, size_t* quad_count, float* units, size_t* unit_count) {
+    MirrorHost m;
+    if (host_mirror(s, &m) != 0) return -1;
+    *quad_count = m.quads.size() / 28;
+    *unit_count = m.units.size() / 16;
+    if (quads) std::memcpy(quads, m.quads.data(), m.quads.size() * 4);
+    if (units) std::memcpy(units, m.units.data(), m.units.size() * 4);
+    return 0;
+}
 void rt_scene_build(rt_scene* s) { s->scene.BuildHost(); }
 void rt_scene_camera(const rt_scene* s, GPUCamera* out) {
     *out = static_cast<const GPUCamera&>(const_cast<Scene&>(s->scene).GetCamera());

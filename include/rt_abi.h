@@ -487,6 +487,9 @@ int rt_twin_check_host(const float rec[12], const float origin[3], const float n
    aligned in right-first pre-order), built on the host: *count receives the node count; nodes (may
    be NULL) receives the records.  0 or -1 with rt_last_error(). */
 int rt_scene_mirror_nodes(rt_scene* scene, GPUBVHNode* nodes, size_t* count);
+/* The big leaves' twin records (mirror.h quads: 28 floats each, units: 16 floats each), built on the
+   host: counts first, then the arrays when the pointers are not NULL.  0 or -1. */
+int rt_scene_mirror_twins(rt_scene* scene, float* quads, size_t* quad_count, float* units, size_t* unit_count);
 
 /* XORWOW jump matrix A^(4^k * 2^67) (k < 32) as 800 uint32 words in rocrand's layout
  * m[i*160 + j*5 + w] (input word i, bit j, output word w).  For tests. */

@@ -221,3 +221,45 @@ def test_twin_quads_and_bound(which):
             bad += (b & 1) and (b & 2)
     assert bad == 0, f"{bad} twins declared rejected but accepted by glm's predicate"
     assert decided > 0.5 * total, (decided, total)
+
+
+@pytest.mark.parametrize("which", ["bunny", "bunny4"])
+def test_twin_records_cover_every_triangle_once(which):
+    """mirror.h quads / units of every big leaf with pair records: each leaf position appears exactly
+    once, as a unit's triangle or as its twin; a unit record is the leaf's record with the twin's face
+    and packed positions, a twin record is the same v0 with e1 and e2 swapped bit for bit; kd < 0
+    exactly when there is no twin; quads hold the units two by two in the packed-pair layout."""
+    rt = T.load_rt()
+    s = rt.Scene()
+    s.setup(which)
+    s.build()
+    tris = s.mirror()
+    tu = tris.view(np.uint32).reshape(-1, 12)
+    quads, units = s.mirror_twins()
+    qu, uu = quads.view(np.uint32), units.view(np.uint32)
+    nodes = s.host_arrays()["nodes"].view(np.uint32).reshape(-1, 8)
+    counts = {int(n[6]): int(n[7]) for n in nodes if n[7] > 0}
+    leads = [i for i in range(tu.shape[0]) if tu[i, 11] in (1, 3)]
+    assert leads
+    for f in leads:
+        c = counts[f]
+        qb, nq, ub, nu = int(tu[f + 1, 10]), int(tu[f + 1, 11]), int(tu[f + 2, 10]), int(tu[f + 2, 11])
+        assert nq == (nu + 1) // 2
+        seen = []
+        for k in range(nu):
+            r, w = units[ub + k], int(uu[ub + k, 11])
+            pos, twin = w & 0xFFFF, w >> 16
+            assert np.array_equal(uu[ub + k, :10], tu[f + pos, :10])
+            seen.append(pos)
+            if twin != 0xFFFF:
+                seen.append(twin)
+                assert np.array_equal(tu[f + twin, 0:3], uu[ub + k, 0:3])
+                assert np.array_equal(tu[f + twin, 3:6], uu[ub + k, 6:9]) and np.array_equal(tu[f + twin, 6:9], uu[ub + k, 3:6])
+                assert uu[ub + k, 10] == tu[f + twin, 9] and r[12] >= 0
+            else:
+                assert r[12] < 0
+            # the quad holding this unit: half k % 2 of quad k // 2 (pairs layout, mirror.h)
+            q, h = qb + k // 2, k % 2
+            assert qu[q, 0 + h] == uu[ub + k, 0] and qu[q, 18 + h] == uu[ub + k, 9]
+            assert qu[q, 24 + h] == uu[ub + k, 11] and (quads[q, 20 + h] < 0) == (r[12] < 0)
+        assert sorted(seen) == list(range(c)), "every position once"
