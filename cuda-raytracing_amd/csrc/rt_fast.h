@@ -69,17 +69,9 @@ __device__ __forceinline__ void slab_exact(const Ray& R, float4 lo, float4 hi, f
 // Approximate slab: same numerators (b - o, exact as in the reference), quotients by
 // multiplication with RN(1/d).  Only called when R.fast (no NaN / inf / subnormal).
 __device__ __forceinline__ void slab_approx(const Ray& R, float4 lo, float4 hi, float* tmin_o, float* tmax_o) {
-#ifdef RT_PK_SLAB  // A/B (tools/build_variant.sh): the six subtractions / products as packed pairs
-    typedef float p2 __attribute__((ext_vector_type(2)));
-    const p2 ta = (p2{lo.x, lo.y} - p2{R.o.x, R.o.y}) * p2{R.r.x, R.r.y};
-    const p2 tb = (p2{lo.z, lo.w} - p2{R.o.z, R.o.x}) * p2{R.r.z, R.r.x};
-    const p2 tc = (p2{hi.x, hi.y} - p2{R.o.y, R.o.z}) * p2{R.r.y, R.r.z};
-    const float tx1 = ta.x, ty1 = ta.y, tz1 = tb.x, tx2 = tb.y, ty2 = tc.x, tz2 = tc.y;
-#else
     const float tx1 = (lo.x - R.o.x) * R.r.x, tx2 = (lo.w - R.o.x) * R.r.x;
     const float ty1 = (lo.y - R.o.y) * R.r.y, ty2 = (hi.x - R.o.y) * R.r.y;
     const float tz1 = (lo.z - R.o.z) * R.r.z, tz2 = (hi.y - R.o.z) * R.r.z;
-#endif
     *tmin_o = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
     *tmax_o = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
 }
@@ -1117,11 +1109,23 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
                 uint32_t bpos = NO_POS;
                 bool nan = !(h.best == h.best);
                 ConstF4 qs = (ConstF4)(quads + 7 * (size_t)__float_as_uint(l2.z));
+#ifdef RT_QUAD_PREFETCH  // A/B: the next quad's scalar loads issued before this quad's tests
+                Pair P = make_pair(qs[0], qs[1], qs[2], qs[3], qs[4]);
+                f4v bnd = qs[5];
+                for (uint32_t q = 0; q < nq; q++) {
+                    const ConstF4 nx = q + 1 < nq ? qs + 7 : qs;
+                    const Pair Pn = make_pair(nx[0], nx[1], nx[2], nx[3], nx[4]);
+                    const f4v bn = nx[5];
+                    if (waiting) quad_test(R.o, R.nd, P, bnd, qs + 6, h, bpos, nan);
+                    P = Pn, bnd = bn, qs = nx;
+                }
+#else
                 for (uint32_t q = 0; q < nq; q++, qs += 7) {
                     const Pair P = make_pair(qs[0], qs[1], qs[2], qs[3], qs[4]);
                     const f4v bnd = qs[5];
                     if (waiting) quad_test(R.o, R.nd, P, bnd, qs + 6, h, bpos, nan);
                 }
+#endif
                 if (waiting && nan) {  // the sequential loop from the entry distance (never taken for finite scenes)
                     h = h0;
                     leaf_sequential(tris, f0, c0, R.o, R.nd, h);
