@@ -1109,23 +1109,11 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
                 uint32_t bpos = NO_POS;
                 bool nan = !(h.best == h.best);
                 ConstF4 qs = (ConstF4)(quads + 7 * (size_t)__float_as_uint(l2.z));
-#ifdef RT_QUAD_PREFETCH  // A/B: the next quad's scalar loads issued before this quad's tests
-                Pair P = make_pair(qs[0], qs[1], qs[2], qs[3], qs[4]);
-                f4v bnd = qs[5];
-                for (uint32_t q = 0; q < nq; q++) {
-                    const ConstF4 nx = q + 1 < nq ? qs + 7 : qs;
-                    const Pair Pn = make_pair(nx[0], nx[1], nx[2], nx[3], nx[4]);
-                    const f4v bn = nx[5];
-                    if (waiting) quad_test(R.o, R.nd, P, bnd, qs + 6, h, bpos, nan);
-                    P = Pn, bnd = bn, qs = nx;
-                }
-#else
                 for (uint32_t q = 0; q < nq; q++, qs += 7) {
                     const Pair P = make_pair(qs[0], qs[1], qs[2], qs[3], qs[4]);
                     const f4v bnd = qs[5];
                     if (waiting) quad_test(R.o, R.nd, P, bnd, qs + 6, h, bpos, nan);
                 }
-#endif
                 if (waiting && nan) {  // the sequential loop from the entry distance (never taken for finite scenes)
                     h = h0;
                     leaf_sequential(tris, f0, c0, R.o, R.nd, h);
