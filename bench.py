@@ -529,6 +529,30 @@ def refine_lane_map(rt, render, rng, lm, cost, rounds, theta, dev, waves_per_sim
                  "s": round(time.perf_counter() - t0, 3)}
 
 
+def settle_occupancy(probe_occupancy, lane_slots, refine_occ, world, cdev):
+    """The frames' occupancy with this rank's lane map (or None), and whether the map survives.
+    probe_occupancy(map) -> (waves per SIMD, {wps: ms}) times each candidate and max-reduces over ranks,
+    so EVERY rank must make the same probe calls: whether a rank kept its lane map is its own
+    decision (refine_lane_map drops a map that loses to the plain order on its shard), so the re-probe
+    of the plain order below runs when ANY rank holds a map (a MAX-reduced flag), and when the plain
+    order wins every rank drops its map.  Returns (wps, best, lane_slots, note or None)."""
+    import torch
+    import torch.distributed as dist
+
+    wps, best = probe_occupancy(lane_slots)
+    any_map = lane_slots is not None
+    if world > 1:
+        t = torch.tensor([1 if any_map else 0], dtype=torch.int32, device=cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        any_map = bool(t.item())
+    if any_map and refine_occ is not None and wps != refine_occ:
+        # a map was kept against the plain order at another occupancy: compare again at this one
+        plain_wps, plain_best = probe_occupancy(None)
+        if plain_best[plain_wps] <= best[wps]:
+            return plain_wps, plain_best, None, f"dropped at {wps} waves per SIMD (the plain tile order is faster)"
+    return wps, best, lane_slots, None
+
+
 def run(args):
     import torch
     import torch.distributed as dist
@@ -541,11 +565,15 @@ def run(args):
     wd.phase = "scene set-up and plans"
     assert world == args.gpus or args.pmc_child, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     rt = G.load_package()
-    if args.tracer != "fast" or args.refill or (args.tune & 0x1030):
-        rt.load_experimental()  # A/B render paths (librt_hip_exp.so); the production path never needs it
-    if args.build_options:  # exact-preserving mirror / BVH builder knobs (rt_set_build_options)
-        rt.set_build_options(**{k: float(v) if k == "split_angle" else int(v)
-                                for k, v in (kv.split("=") for kv in args.build_options.split(","))})
+    build_opts = {k: float(v) if k == "split_angle" else int(v)
+                  for k, v in (kv.split("=") for kv in args.build_options.split(","))} if args.build_options else {}
+    # A/B render paths (librt_hip_exp.so; the production path never needs it): the tracers, refill, the
+    # RT_TUNE A/B families, and the big-leaf screen variants a mirror with screen records asks for
+    # (rt_kernel.hip needs_experimental)
+    if args.tracer != "fast" or args.refill or (args.tune & 0x1030) or build_opts.get("leaf_screens", 0):
+        rt.load_experimental()
+    if build_opts:  # exact-preserving mirror / BVH builder knobs (rt_set_build_options)
+        rt.set_build_options(**build_opts)
     scene_name, W, H, SPP, BOUNCES, desc = CONFIGS[args.config]
     if world > 1 and args.scaling == "weak":
         W, H = weak_size(W, H, world)
@@ -673,16 +701,11 @@ def run(args):
 
     if auto_occ:
         t1 = time.perf_counter()
-        occupancy["waves_per_simd"], best = probe_occupancy(lane_slots)
-        if lane_slots is not None and refine_occ is not None and occupancy["waves_per_simd"] != refine_occ:
-            # the map was kept against the plain order at another occupancy: compare again at this one
-            wps = occupancy["waves_per_simd"]
-            plain_wps, plain_best = probe_occupancy(None)
-            if plain_best[plain_wps] <= best[wps]:
-                lane_slots = None
-                occupancy["waves_per_simd"] = plain_wps
-                plan_info["lanes"]["map"] = f"dropped at {wps} waves per SIMD (the plain tile order is faster)"
-                best = plain_best
+        cdev = dev if world > 1 and dist.get_backend() == "nccl" else torch.device("cpu")
+        occupancy["waves_per_simd"], best, lane_slots, note = settle_occupancy(probe_occupancy, lane_slots, refine_occ,
+                                                                               world, cdev)
+        if note:
+            plan_info["lanes"]["map"] = note
         setup_s += time.perf_counter() - t1
         plan_info = dict(plan_info or {}, occupancy={"waves_per_simd": occupancy["waves_per_simd"],
                                                      "probe_ms": {str(k): round(v, 3) for k, v in best.items()},

@@ -156,6 +156,7 @@ SIGNATURES = {
     "rt_scene_mirror_copy": (_I, [_P, _P, _P, _P]),
     "rt_scene_mirror_nodes": (_I, [_P, _P, ctypes.POINTER(_SZ)]),
     "rt_scene_mirror_twins": (_I, [_P, _P, ctypes.POINTER(_SZ), _P, ctypes.POINTER(_SZ)]),
+    "rt_mirror_build_check": (_I, [_P, _SZ, _P, _SZ, _P, _SZ, _P, _SZ, _P, ctypes.POINTER(ctypes.c_int)]),
     "rt_cluster_cull_host": (_I, [_P, _P, ctypes.c_float, _P]),
     "rt_twin_check_host": (_I, [_P, _P, _P]),
     "rt_xorwow_jump_matrix": (_I, [_I, ctypes.POINTER(ctypes.c_uint32)]),
@@ -199,7 +200,8 @@ def load_experimental():
             raise RTError(f"{EXP_LIB_PATH} not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
         _exp_lib = ctypes.CDLL(EXP_LIB_PATH)
     if lib().rt_experimental_loaded() != 1:
-        raise RTError("librt_hip_exp.so loaded but its kernels are not registered with librt_hip.so")
+        raise RTError("librt_hip_exp.so loaded but its kernels are not registered with librt_hip.so: "
+                      + lib().rt_last_error().decode(errors="replace"))
     return _exp_lib
 
 
@@ -351,6 +353,21 @@ class Scene:
         nn, nf, nv = counts[0].value, counts[1].value, counts[2].value
         return {"nodes": grab(ptrs[0], nn * 32), "face_indices": grab(ptrs[1], nf * 4),
                 "vertices": grab(ptrs[2], nv * 32), "faces": grab(ptrs[3], nf * 16)}
+
+
+def mirror_build_check(nodes, face_indices, faces, vertices):
+    """rt_mirror_build_check: the host mirror of raw reference arrays (numpy: nodes (N,8) 32-bit, face
+    indices u32, faces (F,4) u32, vertices (V,8) f32) -> (words 10-11 of every record as (n, 2) uint32,
+    whether twin records were built)."""
+    import numpy as np
+    nodes, fi = np.ascontiguousarray(nodes), np.ascontiguousarray(face_indices, dtype=np.uint32)
+    faces, vertices = np.ascontiguousarray(faces), np.ascontiguousarray(vertices)
+    meta = np.zeros((fi.size, 2), dtype=np.uint32)
+    tw = ctypes.c_int(0)
+    _check(lib().rt_mirror_build_check(nodes.ctypes.data, nodes.shape[0], fi.ctypes.data, fi.size, faces.ctypes.data,
+                                       faces.shape[0], vertices.ctypes.data, vertices.shape[0], meta.ctypes.data,
+                                       ctypes.byref(tw)), "rt_mirror_build_check")
+    return meta, bool(tw.value)
 
 
 def bvh_build_device(vertices, faces, stream=None):

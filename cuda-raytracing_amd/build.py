@@ -8,6 +8,7 @@ liboracle.so   oracle/rt_oracle.c        -> the CPU restatement used only by tes
 Both are built in-tree so the built .so files travel to the GPU box with the repo snapshot.
 """
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -29,13 +30,13 @@ ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 FP_FLAGS = ["-ffp-contract=off", "-fno-fast-math"]
 # Device code generation: branches on wave-uniform conditions stay scalar branches instead of being
 # structurized like divergent ones (config 2: 15.65 vs 15.93 ms per frame, three interleaved runs
-# on one box, tools/build_variant.sh + tools/gpu_variants.sh; config 4 unchanged).
-HIP_CODEGEN_FLAGS = ["-mllvm", "-structurizecfg-skip-uniform-regions=1"]
-# ... except for the 6-wave kernels: each render family below is compiled twice, once with the option
-# and its 6-wave kernels sent to a second unit (RT_W6_SPLIT), once without the option holding only those
-# (RT_W6_ONLY) -- the 6-wave leaf-tree kernel was miscompiled under the option (rt_fast_body.h)
-W6_SPLIT = {"rt_fast_prod.hip", "rt_fast_timing.hip", "rt_fast_ab.hip", "rt_fast_ab2.hip", "rt_fast_refill.hip",
-            "rt_fast_screen.hip"}
+# on one box, tools/build_variant.sh + tools/gpu_variants.sh; config 4 unchanged) -- with LLVM's
+# redundant-END_CF removal off: that removal lowers an inner divergent if whose join is its parent's
+# as `s_and_b64 exec, exec, cond` (no saved mask), and the register allocator, which runs after it, may
+# put live-range copies into the flow block behind it, which the lanes turned off then skip.  Together
+# with the first option it corrupted the 6-wave leaf-tree kernel (rt_fast_body.h);
+# check_exec_narrowing below guards every object against that pattern.
+HIP_CODEGEN_FLAGS = ["-mllvm", "-structurizecfg-skip-uniform-regions=1", "-mllvm", "-amdgpu-remove-redundant-endcf=0"]
 HOST_SOURCES = ["scene.cpp", "objload.cpp", "mirror.cpp", "leaftree.cpp", "xorwow.cpp", "image.cpp", "shard.cpp"]
 # the render kernel families compile as separate translation units, in parallel (rt_render.h)
 HIP_SOURCES = ["rt_fast_prod.hip", "rt_fast_timing.hip", "rt_fast_stats.hip", "rt_ref.hip", "rt_kernel.hip", "image.hip",
@@ -64,17 +65,89 @@ def _deps(dirpath, exts):
     return [os.path.join(dirpath, f) for f in os.listdir(dirpath) if f.endswith(exts)]
 
 
-def _hip_job(src, w6=None):
-    """w6: None (a plain unit), "split" (RT_W6_SPLIT) or "only" (RT_W6_ONLY, without the codegen option)."""
-    obj = os.path.join(BUILD, src + (".w6.o" if w6 == "only" else ".o"))
-    extra = {None: HIP_CODEGEN_FLAGS, "split": HIP_CODEGEN_FLAGS + ["-DRT_W6_SPLIT"], "only": ["-DRT_W6_ONLY"]}[w6]
+def _hip_job(src):
+    obj = os.path.join(BUILD, src + ".o")
     return obj, [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *FP_FLAGS,
-                 "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics", "-fno-slp-vectorize", *extra,
-                 "-I", INC, "-I", CSRC, "-c", os.path.join(CSRC, src), "-o", obj]
+                 "-fhip-fp32-correctly-rounded-divide-sqrt", "-munsafe-fp-atomics", "-fno-slp-vectorize",
+                 *HIP_CODEGEN_FLAGS, "-I", INC, "-I", CSRC, "-c", os.path.join(CSRC, src), "-o", obj]
 
 
-def _hip_jobs(src):
-    return [_hip_job(src, "split"), _hip_job(src, "only")] if src in W6_SPLIT else [_hip_job(src)]
+LLVM_BIN = "/opt/rocm/lib/llvm/bin"
+_VECTOR_OP = re.compile(r"\s*(v_|global_|scratch_|buffer_|ds_|flat_)")
+_LANE_OP = re.compile(r"\s*v_(readlane|readfirstlane|writelane)_")  # ignore exec (not a hazard here)
+
+
+def disassemble(obj):
+    """The gfx950 code object inside a HIP object file (.hip_fatbin bundle), disassembled."""
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        fat, co = os.path.join(td, "fat.bin"), os.path.join(td, "dev.co")
+        secs = subprocess.run([f"{LLVM_BIN}/llvm-readelf", "-S", obj], check=True, capture_output=True, text=True).stdout
+        if ".hip_fatbin" not in secs:
+            return ""  # no device code in this unit
+        subprocess.run([f"{LLVM_BIN}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", obj, os.path.join(td, "x.o")],
+                       check=True, capture_output=True)
+        subprocess.run([f"{LLVM_BIN}/clang-offload-bundler", "--type=o", f"--targets=hipv4-amdgcn-amd-amdhsa--{ARCH}",
+                        f"--input={fat}", f"--output={co}", "--unbundle"], check=True, capture_output=True)
+        return subprocess.run([f"{LLVM_BIN}/llvm-objdump", "-d", f"--mcpu={ARCH}", co], check=True,
+                              capture_output=True, text=True).stdout
+
+
+def exec_narrowing_hazards(dis):
+    """Vector instructions that run under an exec mask narrowed without a save (`s_and_b64 exec, exec, c`)
+    in the blocks its execz branch skips to, before the parent's `s_or_b64 exec, exec, s` restores the
+    mask: the lanes turned off never run them, although in the thread-level CFG the register allocator
+    sees every lane of the parent region passes through that block (rt_fast_body.h RT_FAST_FAMILY).
+    `dis` is llvm-objdump output; returns [(kernel, narrowing address, [instructions])]."""
+    base, ins = {}, []  # symbol -> address; (address, text, branch target or None, kernel)
+    kernel = None
+    for ln in dis.split("\n"):
+        m = re.match(r"^([0-9a-f]+) <(\S+)>:$", ln)
+        if m:
+            kernel = m.group(2)
+            base[kernel] = int(m.group(1), 16)
+            continue
+        m = re.match(r"^\t(.*?)\s*// ([0-9A-F]+):[0-9A-F ]*(?:<(\S+)\+0x([0-9a-f]+)>)?", ln)
+        if m:
+            tgt = (m.group(3), int(m.group(4), 16)) if m.group(3) else None
+            ins.append((int(m.group(2), 16), m.group(1), tgt, kernel))
+    at = {a: i for i, (a, _, _, _) in enumerate(ins)}
+    out = []
+    for i, (addr, text, _, k) in enumerate(ins):
+        if not text.startswith("s_and_b64 exec, exec,"):
+            continue
+        j, target = i + 1, None
+        while j < len(ins) and not ins[j][1].startswith("s_or_b64 exec, exec,"):
+            if target is None and ins[j][1].startswith("s_cbranch_execz") and ins[j][2]:
+                sym, off = ins[j][2]
+                target = base.get(sym, -1) + off
+            j += 1
+        if target is None:
+            continue
+        if target not in at:
+            out.append((k, addr, ["(execz target not found)"]))
+            continue
+        bad = []
+        for _, tx, _, _ in ins[at[target]:]:
+            if tx.startswith("s_or_b64 exec, exec,") or tx.startswith("s_endpgm"):
+                break
+            if _VECTOR_OP.match(tx) and not _LANE_OP.match(tx):
+                bad.append(tx)
+        if bad:
+            out.append((k, addr, bad))
+    return out
+
+
+def check_exec_narrowing(objs):
+    """Build guard: no HIP object may carry exec_narrowing_hazards (the miscompile of round 4's 6-wave
+    kernel).  Raises RuntimeError naming the kernel and the instructions."""
+    problems = []
+    for obj in objs:
+        for k, addr, bad in exec_narrowing_hazards(disassemble(obj)):
+            problems.append(f"{os.path.basename(obj)}: {k} at 0x{addr:x}: " + "; ".join(bad[:4]))
+    if problems:
+        raise RuntimeError("exec narrowed without a save with vector code behind it (tools/exec_narrow_scan.py, "
+                           "rt_fast_body.h RT_FAST_FAMILY):\n  " + "\n  ".join(problems))
 
 
 def _compile(jobs, force):
@@ -105,14 +178,16 @@ def _compile(jobs, force):
 def build_product(force=False):
     """librt_hip.so and the experimental plugin librt_hip_exp.so (linked against it)."""
     os.makedirs(BUILD, exist_ok=True)
-    jobs = [j for src in HIP_SOURCES for j in _hip_jobs(src)]
+    jobs = [_hip_job(src) for src in HIP_SOURCES]
     for src in HOST_SOURCES:
         obj = os.path.join(BUILD, src + ".o")
         jobs.append((obj, ["g++", "-O2", "-std=c++17", "-fPIC", *FP_FLAGS, "-I", INC, "-I", CSRC,
                            "-c", os.path.join(CSRC, src), "-o", obj]))
-    exp_jobs = [j for src in EXP_SOURCES for j in _hip_jobs(src)]
+    exp_jobs = [_hip_job(src) for src in EXP_SOURCES]
     changed = _compile(jobs + exp_jobs, force)
     objs = [o for o, _ in jobs]
+    if changed:
+        check_exec_narrowing([o for o, _ in jobs + exp_jobs if o.endswith(".hip.o")])
     if changed or not _newer(LIB, objs):
         tmp = LIB + ".tmp"
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-L/opt/rocm/lib", "-lrccl", "-o", tmp])

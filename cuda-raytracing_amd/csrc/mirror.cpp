@@ -181,6 +181,27 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
     }
     std::sort(big.begin(), big.end());
     big.erase(std::unique(big.begin(), big.end()), big.end());
+    // A big leaf's metadata lives in words 10-11 of its records: the first (po, pf), the second and third
+    // (its quads, its units: the twins).  The kernel reads the second and third of every big leaf with pair
+    // records, so they must belong to that leaf alone -- neither another big leaf's first record nor its
+    // second / third.  A BVH from the reference's builder never violates this (a leaf range is one node's),
+    // but a foreign BVH whose big-leaf ranges overlap with different starts could: such a scene gets no
+    // twins at all (pairs only, exact either way) instead of records that overwrite each other.
+    bool twins_ok = true;
+    {
+        std::vector<uint8_t> role(index_count, 0);  // 1: a big leaf's first record, 2: a big leaf's second / third
+        for (uint32_t n : big) role[nodes[n].first_index] = 1;
+        std::vector<uint32_t> firsts;
+        for (uint32_t n : big) firsts.push_back(nodes[n].first_index);
+        std::sort(firsts.begin(), firsts.end());
+        firsts.erase(std::unique(firsts.begin(), firsts.end()), firsts.end());
+        for (uint32_t f : firsts)
+            for (size_t r = (size_t)f + 1; r <= (size_t)f + 2 && twins_ok; r++) {
+                if (r >= index_count || role[r] != 0) twins_ok = false;
+                else role[r] = 2;
+            }
+    }
+    out->twins = twins_ok;
     std::vector<uint32_t> roots;
     for (uint32_t n : big) {
         const GPUBVHNode& nd = nodes[n];
@@ -230,7 +251,7 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
         // the twins; the leaf's second / third record say where its quads / units are (mirror.h)
         const uint32_t qb = (uint32_t)(out->quads.size() / 28), ub = (uint32_t)(out->units.size() / 16);
         uint32_t nq = 0, nu = 0;
-        if (build_twins(out->tris.data(), nd.first_index, nd.prim_count, out->quads, out->units, &nq, &nu)) {
+        if (twins_ok && build_twins(out->tris.data(), nd.first_index, nd.prim_count, out->quads, out->units, &nq, &nu)) {
             float* second = &out->tris[((size_t)nd.first_index + 1) * 12];
             float* third = &out->tris[((size_t)nd.first_index + 2) * 12];
             std::memcpy(&second[10], &qb, 4);
@@ -468,6 +489,21 @@ rt_build_options default_options() {
 }
 rt_build_options g_options = default_options();
 }  // namespace
+
+extern "C" int rt_mirror_build_check(const GPUBVHNode* nodes, size_t node_count, const uint32_t* face_indices,
+                                     size_t index_count, const GPUFace* faces, size_t face_count,
+                                     const GPUVertex* vertices, size_t vertex_count, uint32_t* meta, int* twins) {
+    try {
+        MirrorHost m;
+        rt_build_mirror(nodes, node_count, face_indices, index_count, faces, face_count, vertices, vertex_count, &m);
+        for (size_t i = 0; i < index_count; i++) std::memcpy(&meta[2 * i], &m.tris[i * 12 + 10], 8);
+        *twins = m.twins && !m.quads.empty() ? 1 : 0;
+        return 0;
+    } catch (const std::exception& e) {
+        rt_internal_set_error(e.what());
+        return -1;
+    }
+}
 
 extern "C" void rt_get_build_options(rt_build_options* out) {
     if (!out) return;

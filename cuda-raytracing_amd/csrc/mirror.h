@@ -76,6 +76,7 @@ struct MirrorHost {
     int depth = 0;                // deepest leaf (root = 0) reachable from node 0
     bool fast = true;             // node bounds inside the filtered-slab range (rt_fast.h)
     int screens = 0;              // big leaves with a screen record (pf = 3)
+    bool twins = true;            // false: big-leaf metadata records would collide (overlapping leaves), no twins
 };
 
 // Build from host copies of the reference arrays.  node_count / face_count / vertex_count

@@ -8,10 +8,10 @@ namespace rtk {
 namespace {
 const ExperimentalKernels kTable{launch_fast_ab, launch_fast_refill, launch_lone, launch_wavefront, launch_fast_screen};
 struct Registrar {
-    Registrar() { register_experimental_kernels(&kTable); }
-    ~Registrar() { register_experimental_kernels(nullptr); }
+    Registrar() { register_experimental_kernels(&kTable, kExperimentalAbi); }
+    ~Registrar() { register_experimental_kernels(nullptr, kExperimentalAbi); }
 } registrar;
 }  // namespace
 }  // namespace rtk
 
-extern "C" int rt_exp_abi_version() { return 1; }
+extern "C" int rt_exp_abi_version() { return (int)rtk::kExperimentalAbi; }

@@ -18,10 +18,8 @@ hipError_t launch_fast_ab2(int stack, int mode, const RenderArgs& a, int waves, 
 hipError_t launch_fast_ab1(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s);
 RT_FAST_FAMILY(launch_fast_ab1, dispatch)
 
-#if !defined(RT_W6_ONLY)
 hipError_t launch_fast_ab(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s) {
     return (mode == 2 || mode == 0) ? launch_fast_ab2(stack, mode, a, waves, s) : launch_fast_ab1(stack, mode, a, waves, s);
 }
-#endif
 
 }  // namespace rtk

@@ -433,18 +433,9 @@ hipError_t launch_grid(K kernel, const RenderArgs& args, int waves, bool refill,
 // One (STACK, STATS, MODE) variant at the occupancy rt_render_params asks for: statistics frames run
 // the unconstrained kernel; the others 5 waves per SIMD (default), 6 or 7 (waves_per_simd, or
 // RT_TUNE bits 9-10 = 2 / 3).  rt_render rejects the retired RT_TUNE override 1 (compiler's choice).
-#if defined(RT_W6_ONLY)
-// the 6-wave unit's launcher has a name of its own: the two units of a family must not both define
-// launch_occ<...> (an inline template, so the linker would keep one body for both)
-#define launch_occ launch_occ_w6_unit
-#endif
 template <int STACK, bool STATS, int MODE>
 hipError_t launch_occ(const RenderArgs& args, int waves, hipStream_t stream) {
     constexpr bool refill = (MODE & 64) != 0;  // only these variants drain a refill queue
-#if defined(RT_W6_ONLY)
-    static_assert(!STATS, "statistics families have no 6-wave kernels");
-    return launch_grid(render_fast_kernel_w6<STACK, false, MODE>, args, waves, refill, stream);
-#else
     if constexpr (STATS) {
         return launch_grid(render_fast_kernel<STACK, true, MODE>, args, waves, refill, stream);
     } else {
@@ -455,51 +446,31 @@ hipError_t launch_occ(const RenderArgs& args, int waves, hipStream_t stream) {
             return launch_grid(k, args, waves, refill, stream, cap_lds_bytes(k, w), w);
         }
         if (w == 7) return launch_grid(render_fast_kernel_w7<STACK, false, MODE>, args, waves, refill, stream);
-#if defined(RT_W6_SPLIT)
-        if (w == 6) return hipErrorInvalidValue;  // the family entry sends these to its _w6 unit
-#else
         if (w == 6) return launch_grid(render_fast_kernel_w6<STACK, false, MODE>, args, waves, refill, stream);
-#endif
         return launch_grid(render_fast_kernel_w5<STACK, false, MODE>, args, waves, refill, stream);
     }
-#endif
-}
-
-// Whether a frame runs the 6-wave kernel of its family (launch_occ's choice for the non-statistics
-// families).
-inline bool wants_w6(const RenderArgs& a) {
-    const uint32_t t = (a.tune >> 9) & 3u;
-    return t == 2u || (t == 0u && a.waves_per_simd == 6);
 }
 
 // A family's entry point: the stack size (30 / 40 / 64 entries) picks the instantiation.
 //
-// The 6-wave kernels of a family are compiled in a translation unit of their own (build.py: the same
-// source with RT_W6_ONLY, as NAME_w6, without -structurizecfg-skip-uniform-regions): with that option
-// the 6-wave build of the leaf-tree kernel rendered wrong pixels three times this round, each time after
-// an unrelated code change (a variant that never ran its new code, a screen-record mirror), while the
-// same source without the option, and the 5- and 7-wave builds with it, matched the oracle bit for bit
-// (tools/variant_agree.py ORACLE=1; tests/test_gpu_fullframe.py covers every occupancy).  The 5- and
-// 7-wave kernels keep the option: it is worth ~6 % on config 2 (13.8 vs 14.7 ms, round 4).
-#define RT_FAST_SWITCH(DISPATCH) \
-    switch (stack) { \
-        case 30: return DISPATCH<30>(mode, a, waves, s); \
-        case 40: return DISPATCH<40>(mode, a, waves, s); \
-        default: return DISPATCH<64>(mode, a, waves, s); \
-    }
-#if defined(RT_W6_ONLY)
+// Every unit is compiled with -structurizecfg-skip-uniform-regions AND -amdgpu-remove-redundant-endcf=0
+// (build.py).  Round 4 found the 6-wave leaf-tree kernel rendering wrong pixels under the first option;
+// round 5 traced it (tools/w6_repro.sh): LLVM's redundant-END_CF removal lowered the
+// divergent early return of cluster_cull (`if (!(dlb > ...)) return false`) inside coop_tree as
+// `s_and_b64 exec, exec, vcc` with no saved mask, the parent if's `s_or_b64 exec` restoring it; the
+// register allocator, running after that lowering, then put a live-range copy of the lane's ray origin
+// (v[60:63] <- v[74:77]) into the flow block behind it, which the lanes that failed the test skip -- and
+// bb.406 had just loaded the cluster record into v[60:63] for them.  A uniform branch left unstructurized
+// by the first option (cluster_cull's `best == best` test) added the second path into the join that made
+// the copy necessary.  build.py's guard rejects any object with vector instructions in such a narrowed
+// flow block.
 #define RT_FAST_FAMILY(NAME, DISPATCH) \
-    hipError_t NAME##_w6(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s) { RT_FAST_SWITCH(DISPATCH) }
-#elif defined(RT_W6_SPLIT)
-#define RT_FAST_FAMILY(NAME, DISPATCH) \
-    hipError_t NAME##_w6(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s); \
     hipError_t NAME(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s) { \
-        if (wants_w6(a)) return NAME##_w6(stack, mode, a, waves, s); \
-        RT_FAST_SWITCH(DISPATCH) \
+        switch (stack) { \
+            case 30: return DISPATCH<30>(mode, a, waves, s); \
+            case 40: return DISPATCH<40>(mode, a, waves, s); \
+            default: return DISPATCH<64>(mode, a, waves, s); \
+        } \
     }
-#else
-#define RT_FAST_FAMILY(NAME, DISPATCH) \
-    hipError_t NAME(int stack, int mode, const RenderArgs& a, int waves, hipStream_t s) { RT_FAST_SWITCH(DISPATCH) }
-#endif
 
 }  // namespace rtk

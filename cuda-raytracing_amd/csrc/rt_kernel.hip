@@ -268,7 +268,16 @@ hipError_t launch_fast(const RenderArgs& args, int waves, int depth, bool stats,
 
 }  // namespace
 
-void rtk::register_experimental_kernels(const rtk::ExperimentalKernels* k) { g_experimental.store(k); }
+void rtk::register_experimental_kernels(const rtk::ExperimentalKernels* k, uint32_t abi) {
+    if (k && abi != rtk::kExperimentalAbi) {  // a plugin built against another RenderArgs / table layout
+        char msg[160];
+        std::snprintf(msg, sizeof msg, "librt_hip_exp.so refused: its ABI stamp 0x%08x is not librt_hip.so's 0x%08x "
+                      "(rebuild both)", abi, rtk::kExperimentalAbi);
+        set_error(msg);
+        return;
+    }
+    g_experimental.store(k);
+}
 const rtk::ExperimentalKernels* rtk::experimental_kernels() { return g_experimental.load(); }
 
 namespace {

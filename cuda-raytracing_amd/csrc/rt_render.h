@@ -35,8 +35,13 @@ struct ExperimentalKernels {
     decltype(&launch_wavefront) wavefront;
     decltype(&launch_fast_screen) fast_screen;
 };
-// rt_kernel.hip: the registered table (nullptr until librt_hip_exp.so is loaded).
-void register_experimental_kernels(const ExperimentalKernels* k);
+// Layout stamp of what the plugin shares with librt_hip.so (RenderArgs by reference, this table): a
+// version bumped by hand when a field changes meaning, and the two sizes.  A plugin built against another
+// layout is refused at registration instead of reading a different struct (rt_exp_abi_version).
+constexpr uint32_t kExperimentalAbi = (2u << 24) ^ ((uint32_t)sizeof(RenderArgs) << 8) ^ (uint32_t)sizeof(ExperimentalKernels);
+// rt_kernel.hip: the registered table (nullptr until librt_hip_exp.so is loaded); a table whose `abi` is
+// not this library's kExperimentalAbi is refused (rt_last_error says so, rt_experimental_loaded stays 0).
+void register_experimental_kernels(const ExperimentalKernels* k, uint32_t abi);
 const ExperimentalKernels* experimental_kernels();
 
 }  // namespace rtk

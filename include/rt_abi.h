@@ -491,6 +491,15 @@ int rt_scene_mirror_nodes(rt_scene* scene, GPUBVHNode* nodes, size_t* count);
    host: counts first, then the arrays when the pointers are not NULL.  0 or -1. */
 int rt_scene_mirror_twins(rt_scene* scene, float* quads, size_t* quad_count, float* units, size_t* unit_count);
 
+/* Test hook: the private mirror built on the host from raw reference arrays (the foreign-scene path,
+   rt_render on a GPUScene not uploaded by rt_scene_upload): words 10-11 of every leaf-ordered record --
+   a big leaf's first record (first pair, kind), second and third (its twin quads, its units) -- as
+   2 x index_count uint32 in `meta`, and whether twin records were built (0 when big-leaf ranges overlap
+   so that their metadata records would collide).  0 or -1 (rt_last_error). */
+int rt_mirror_build_check(const GPUBVHNode* nodes, size_t node_count, const uint32_t* face_indices, size_t index_count,
+                          const GPUFace* faces, size_t face_count, const GPUVertex* vertices, size_t vertex_count,
+                          uint32_t* meta, int* twins);
+
 /* XORWOW jump matrix A^(4^k * 2^67) (k < 32) as 800 uint32 words in rocrand's layout
  * m[i*160 + j*5 + w] (input word i, bit j, output word w).  For tests. */
 int rt_xorwow_jump_matrix(int k, uint32_t out[800]);

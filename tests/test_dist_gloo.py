@@ -267,3 +267,63 @@ def test_gather_bookkeeping_uneven_shards(world):
     img, seen = unshard_host(gathered.reshape(world, cap * 256, 4), w, h, lists)
     assert (seen == 1).all()
     assert np.array_equal(img, frame)
+
+
+def _occ_worker(rank, world, port, maps, times, plain_times, result_q):
+    """One rank of bench.settle_occupancy: `maps[rank]` says whether this rank kept its lane map;
+    the fake probe max-reduces its per-candidate times over ranks exactly as bench's does."""
+    import bench
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cands = (3, 4, 5, 6, 7)
+        calls = []
+
+        def probe(ls):
+            calls.append("map" if ls is not None else "plain")
+            src = times if ls is not None else plain_times
+            t = torch.tensor([src[rank][w] for w in cands], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            best = {w: float(x) for w, x in zip(cands, t.tolist())}
+            return min(best, key=best.get), best
+
+        lane_slots = np.arange(64, dtype=np.int32) if maps[rank] else None
+        wps, best, ls, note = bench.settle_occupancy(probe, lane_slots, 6, world, torch.device("cpu"))
+        dist.barrier()
+        result_q.put((rank, wps, ls is not None, note, calls))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("plain_wins", [True, False])
+def test_occupancy_settles_when_one_rank_dropped_its_map(plain_wins):
+    """refine_lane_map keeps or drops a rank's lane map on that rank alone, so
+    ranks can disagree on `lane_slots is not None`; the plain-order re-probe (a collective) must then
+    run on EVERY rank or the job hangs.  Rank 0 keeps a map, rank 1 dropped its own; the job's
+    occupancy (7, max over ranks) differs from the one the map was refined at (6), so the plain order
+    is probed again on both ranks, and both take the same decision."""
+    world = 2
+    slow = {3: 9.0, 4: 9.0, 5: 8.0}
+    map0 = {**slow, 6: 7.5, 7: 7.0}     # rank 0 with its map
+    plain1 = {**slow, 6: 6.4, 7: 7.2}   # rank 1 (no map): its plain order, first probe and re-probe
+    plain0 = {**slow, **({6: 6.5, 7: 7.9} if plain_wins else {6: 7.8, 7: 7.9})}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_occ_worker, args=(r, world, port, [True, False], [map0, plain1], [plain0, plain1], q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, w0, m0, n0, c0), (r1, w1, m1, n1, c1) = got
+    assert c0 == ["map", "plain"] and c1 == ["plain", "plain"], "both ranks make the same collective calls"
+    assert w0 == w1 == (6 if plain_wins else 7)
+    if plain_wins:
+        assert not m0 and not m1 and n0 and "dropped" in n0 and n1 == n0
+    else:
+        assert m0 and not m1 and n0 is None and n1 is None

@@ -263,3 +263,33 @@ def test_twin_records_cover_every_triangle_once(which):
             assert qu[q, 0 + h] == uu[ub + k, 0] and qu[q, 18 + h] == uu[ub + k, 9]
             assert qu[q, 24 + h] == uu[ub + k, 11] and (quads[q, 20 + h] < 0) == (r[12] < 0)
         assert sorted(seen) == list(range(c)), "every position once"
+
+
+def test_overlapping_big_leaves_get_no_twins():
+    """a big leaf's twin metadata sits in words 10-11 of its second and third records.  A
+    foreign BVH whose big-leaf ranges overlap with different starts would let one leaf's metadata overwrite
+    another's first record; rt_build_mirror then builds no twins at all (pairs only, exact either way), and
+    every big leaf's first record keeps its own (first pair, kind).  The reference's own tree builds twins."""
+    rt = T.load_rt()
+    s = rt.Scene()
+    s.setup("bunny")
+    s.build()
+    arr = s.host_arrays()
+    nodes = arr["nodes"].view(np.uint32).reshape(-1, 8).copy()
+    fi = arr["face_indices"].view(np.uint32)
+    faces = arr["faces"].view(np.uint32).reshape(-1, 4)
+    verts = arr["vertices"].view(np.float32).reshape(-1, 8)
+    meta, twins = rt.mirror_build_check(nodes, fi, faces, verts)
+    assert twins
+    assert np.array_equal(meta, s.mirror().view(np.uint32).reshape(-1, 12)[:, 10:12])
+    big = [int(n[6]) for n in nodes if n[7] > 8]
+    assert big
+    f = big[0]
+    # a small leaf re-pointed at [f + 1, f + 21): a second big leaf starting at the first one's second record
+    small = next(i for i, n in enumerate(nodes) if 0 < n[7] <= 8)
+    nodes[small, 6], nodes[small, 7] = f + 1, 20
+    meta2, twins2 = rt.mirror_build_check(nodes, fi, faces, verts)
+    assert not twins2
+    for lead in (f, f + 1):
+        assert meta2[lead, 1] in (1, 3), f"big leaf at {lead} lost its first-record kind"
+    assert meta2[f, 0] != meta2[f + 1, 0], "each big leaf points at its own pairs"
