@@ -266,7 +266,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
         }
         const rtfast::Ray R = rtfast::make_ray(ro, rd, nd, scene_fast);
         rtfast::trace<STATS, MODE>(nodes4, tris, a.pairs, a.tree, a.ltris, a.flat, a.spairs, a.tune, stk, scratch, R, h,
-                                   path, c, a.quads, a.units);
+                                   path, c, a.quads, a.units, a.two_level != 0);
         if (!path) continue;
 
         bool end = shade_segment<STATS>(a, h, ro, rd, nd, rng, color, thr, c);
@@ -294,6 +294,9 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
             const unsigned long long o = __shfl_xor(lane_max, off);
             lane_max = o > lane_max ? o : lane_max;
         }
+    unsigned long long lane_sum = c.l_small;  // the wave's lane-steps in small-step iterations (timing frame)
+    if ((MODE & 8) && a.stats)
+        for (int off = 32; off > 0; off >>= 1) lane_sum += __shfl_xor(lane_sum, off);
     if ((MODE & 8) && a.stats && threadIdx.x == 0) {  // timing frame: per-wave phase clocks
         atomicAdd(a.stats + RT_STAT_CYCLES_SMALL, c.cy_small);
         atomicAdd(a.stats + RT_STAT_CYCLES_BIG, c.cy_big);
@@ -301,6 +304,8 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
         atomicAdd(a.stats + RT_STAT_ROUNDS_COOP, c.r_coop);
         atomicAdd(a.stats + RT_STAT_ROUNDS_SHARED, c.r_shared);
         atomicAdd(a.stats + RT_STAT_COOP_RAYS, c.coop_rays);
+        atomicAdd(a.stats + RT_STAT_WAVE_SMALL_ITERS, c.w_small);  // small-step wave iterations
+        atomicAdd(a.stats + RT_STAT_LANE_SMALL, lane_sum);          // lane-steps in them
         // cooperative leaf-tree walk (wave-level): rays, subtree + cluster tests, triangle rounds
         atomicAdd(a.stats + RT_STAT_TREE_NODES, c.ktest);
         atomicAdd(a.stats + RT_STAT_TREE_TRI_TESTS, c.ktri);
