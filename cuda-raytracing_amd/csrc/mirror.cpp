@@ -264,7 +264,7 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
     const uint32_t nl = (uint32_t)(out->ltris.size() / 12);
     for (uint32_t r : roots) std::memcpy(&out->tree[(size_t)r * 16 + 12], &nl, 4);
     rt_build_treelets(nodes, node_count, out->treelets);
-    out->nested = rt_build_private_nodes(nodes, node_count, out->nodes);
+    rt_build_private_nodes(nodes, node_count, out->nodes);
 }
 
 // The traversal's private node array (mirror.h nodes): the reference's BVH nodes renumbered so
@@ -276,20 +276,12 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
 // 3 + 2p; an inner node's first_index is its left child's slot, a leaf's is unchanged (the
 // triangle range the tris / pair records are indexed by).  Same boxes, same visit order: the
 // traversal's decisions are the reference's.
-bool rt_build_private_nodes(const GPUBVHNode* nodes, size_t node_count, std::vector<float>& out) {
+void rt_build_private_nodes(const GPUBVHNode* nodes, size_t node_count, std::vector<float>& out) {
     out.clear();
-    if (node_count == 0) return false;
+    if (node_count == 0) return;
     std::vector<uint32_t> slot(node_count, ~0u);  // private slot of every reachable node
     slot[0] = 0;
     uint32_t pairs = 0;
-    bool nested = true;
-    auto inside = [](const GPUBVHNode& c, const GPUBVHNode& p) {
-        for (int k = 0; k < 3; k++)
-            if (!(std::isfinite(c.bmin[k]) && std::isfinite(c.bmax[k]) && c.bmin[k] <= c.bmax[k] && c.bmin[k] >= p.bmin[k] &&
-                  c.bmax[k] <= p.bmax[k]))
-                return false;
-        return true;
-    };
     std::vector<uint32_t> st{0u};
     while (!st.empty()) {  // pre-order, right child first: the order pairs are numbered in
         const uint32_t v = st.back();
@@ -299,18 +291,16 @@ bool rt_build_private_nodes(const GPUBVHNode* nodes, size_t node_count, std::vec
         const uint32_t l = nd.first_index, r = nd.first_index + 1;
         slot[l] = 2 + 2 * pairs, slot[r] = 3 + 2 * pairs;
         pairs++;
-        nested = nested && inside(nodes[l], nd) && inside(nodes[r], nd);
         st.push_back(l);
         st.push_back(r);  // popped first
     }
-    out.assign((size_t)(2 + 2 * pairs + 6) * 8, 0.0f);
+    out.assign((size_t)(2 + 2 * pairs) * 8, 0.0f);
     for (size_t v = 0; v < node_count; v++) {
         if (slot[v] == ~0u) continue;
         GPUBVHNode nd = nodes[v];
         if (nd.prim_count == 0) nd.first_index = slot[nd.first_index];
         std::memcpy(&out[(size_t)slot[v] * 8], &nd, sizeof nd);
     }
-    return nested;
 }
 
 std::vector<float> rt_ltris_device_layout(const std::vector<float>& ltris) {
@@ -442,7 +432,6 @@ int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owne
     e.dev.units = at(9);
     e.dev.depth = m.depth;
     e.dev.fast = m.fast;
-    e.dev.nested = m.nested;
     e.dev.screens = m.screens;
     e.dev.owned = owned;
     e.dev.fingerprint = fingerprint;

@@ -77,7 +77,6 @@ struct MirrorHost {
     bool fast = true;             // node bounds inside the filtered-slab range (rt_fast.h)
     int screens = 0;              // big leaves with a screen record (pf = 3)
     bool twins = true;            // false: big-leaf metadata records would collide (overlapping leaves), no twins
-    bool nested = false;          // private nodes: every child box inside its parent's, all finite (two-level steps)
 };
 
 // Build from host copies of the reference arrays.  node_count / face_count / vertex_count
@@ -96,10 +95,7 @@ void rt_twin_bounds(const float* rec, float* kd, float* ke);
 std::vector<float> rt_ltris_device_layout(const std::vector<float>& ltris);
 
 // The private node array alone (also called by rt_build_mirror).
-// Returns whether every reachable child's box lies inside its parent's (bitwise, finite coordinates): the
-// condition under which rt_fast.h inner_step2 may decide a grandchild without its parent's own test.  The
-// array ends with 6 zero slots, so a step's 128-B load past the last pair stays inside it.
-bool rt_build_private_nodes(const GPUBVHNode* nodes, size_t node_count, std::vector<float>& out);
+void rt_build_private_nodes(const GPUBVHNode* nodes, size_t node_count, std::vector<float>& out);
 
 // The treelets alone (also called by rt_build_mirror).
 void rt_build_treelets(const GPUBVHNode* nodes, size_t node_count, std::vector<float>& out);
@@ -119,7 +115,6 @@ struct MirrorDevice {
     const void* treelets = nullptr;
     int depth = -1;
     bool fast = false;
-    bool nested = false;       // MirrorHost::nested
     int screens = 0;
     bool owned = true;         // built by rt_scene_upload, which forgets it before freeing the arrays
     uint64_t fingerprint = 0;  // foreign scenes: content hash of the arrays it was built from

@@ -247,87 +247,6 @@ __device__ __forceinline__ bool inner_step(const float4* nodes4, const S& stk, i
     return false;
 }
 
-// Two-level inner step (private node array with nested boxes, RenderArgs::two_level).  At inner node N
-// with children L, R the reference pushes L and R and pops R; when R passes and is inner it pushes RL and
-// RR and pops RR -- all with the same `closest`, since no leaf is tested in between
-// (main_raytracing.cu:43-78).  So one step can decide two levels: RR passes -> continue at RR (L and RL
-// pushed); else RL passes -> continue at RL (L pushed); else L decides as in inner_step.  R's own test is
-// not needed when R is inner: a child box lies inside its parent's (the mirror checks it, bitwise, all
-// finite), and IntersectAABB's rounded slab quantities are monotone in the bounds -- per axis RN((b - o) / d)
-// is monotone in b, so the child's tmin is >= the parent's and its tmax <= the parent's (d = +-0 gives
-// +-inf / NaN in the same pattern for both boxes) -- hence a child passing `tmax >= tmin && tmin < closest
-// && tmax > 0` implies the parent passes, and a parent failing makes both children fail, which sends
-// the lane to L exactly as the reference's pop of L after R's rejection.  In the private array R's children
-// pair directly follows the pair of R (mirror.cpp rt_build_private_nodes), so L, R, RL, RR are one 128-B
-// load; R's record says whether RL/RR are its children (R inner with first = first + 2).
-template <bool STATS, class S, class C>
-__device__ __forceinline__ bool inner_step2(const float4* nodes4, const S& stk, int& sp, const Ray& R, float best,
-                                            uint32_t& first, uint32_t& count, C& c) {
-    const float4 l0 = nodes4[2 * first], l1 = nodes4[2 * first + 1];
-    const float4 r0 = nodes4[2 * first + 2], r1 = nodes4[2 * first + 3];
-    const float4 p0 = nodes4[2 * first + 4], p1 = nodes4[2 * first + 5];  // RL (when `two`)
-    const float4 q0 = nodes4[2 * first + 6], q1 = nodes4[2 * first + 7];  // RR
-    if (STATS) c.node += 2;
-    const bool two = __float_as_uint(r1.w) == 0u && __float_as_uint(r1.z) == first + 2u;
-    // X: RR when R is inner, else R itself; Y: RL (only when two)
-    const float4 x0 = two ? q0 : r0, x1 = two ? q1 : r1;
-    float tl = 0.0f, tlx = 0.0f, tx = 0.0f, txx = 0.0f, ty = 0.0f, tyx = 0.0f;
-    int okl = UNSURE, okx = UNSURE, xlt = UNSURE, oky = UNSURE, ylt = UNSURE;
-    if (R.fast) {
-        slab_approx(R, l0, l1, &tl, &tlx);
-        slab_approx(R, x0, x1, &tx, &txx);
-        slab_approx(R, p0, p1, &ty, &tyx);
-        okl = classify_ok(tl, tlx);
-        okx = classify_ok(tx, txx);
-        xlt = okx == YES ? classify_lt(tx, best) : NO;
-        oky = two ? classify_ok(ty, tyx) : NO;
-        ylt = oky == YES ? classify_lt(ty, best) : NO;
-    }
-    bool exact_l = false;
-    if (okl == UNSURE || okx == UNSURE || xlt == UNSURE || oky == UNSURE || (xlt == NO && ylt == UNSURE)) {
-        slab_exact(R, l0, l1, &tl, &tlx);
-        slab_exact(R, x0, x1, &tx, &txx);
-        slab_exact(R, p0, p1, &ty, &tyx);
-        okl = (tlx >= tl && tlx > 0.0f) ? YES : NO;
-        okx = (txx >= tx && txx > 0.0f) ? YES : NO;
-        xlt = (okx == YES && tx < best) ? YES : NO;
-        oky = (two && tyx >= ty && tyx > 0.0f) ? YES : NO;
-        ylt = (oky == YES && ty < best) ? YES : NO;
-        exact_l = true;
-    }
-    if (xlt == YES) {
-        if (okl == YES) stk.put(sp++, first);       // L
-        if (oky == YES) stk.put(sp++, first + 2u);  // RL, above L (pushed at R)
-        first = __float_as_uint(x1.z), count = __float_as_uint(x1.w);
-        return true;
-    }
-    if (ylt == YES) {
-        if (okl == YES) stk.put(sp++, first);
-        first = __float_as_uint(p1.z), count = __float_as_uint(p1.w);
-        return true;
-    }
-    if (okl == YES) {
-        bool llt;
-        if (exact_l) {
-            llt = tl < best;
-        } else {
-            const int cl = classify_lt(tl, best);
-            if (cl == UNSURE) {
-                float te, tx2;
-                slab_exact(R, l0, l1, &te, &tx2);
-                llt = te < best;
-            } else {
-                llt = cl == YES;
-            }
-        }
-        if (llt) {
-            first = __float_as_uint(l1.z), count = __float_as_uint(l1.w);
-            return true;
-        }
-    }
-    return false;
-}
-
 // glm's accept predicate from the four quantities (det, u, v, u + v), as test_triangle.
 __device__ __forceinline__ bool tri_ok(float det, float u, float v, float uv) {
     const float eps = 1.1920928955078125e-07f;
@@ -1100,8 +1019,7 @@ __device__ __forceinline__ bool screen_leaf(const float4* tris, const float4* pa
 // 22.2 vs 20.6 ms, the extra divergence costs more than the saved iterations.)
 template <bool STATS, bool SCR = false, class S, class C>
 __device__ __forceinline__ bool small_step(const float4* nodes4, const float4* tris, const float4* spairs, const S& stk,
-                                           const Ray& R, Hit& h, Trav& T, C& c, const float4* pairs = nullptr,
-                                           bool two_level = false) {
+                                           const Ray& R, Hit& h, Trav& T, C& c, const float4* pairs = nullptr) {
     if constexpr (SCR) {
         if (T.count > (uint32_t)BIG) {  // a big leaf just reached: its screen, else wait for the round
             if (!screen_leaf<STATS>(tris, pairs, R, h, T, c)) {
@@ -1121,12 +1039,7 @@ __device__ __forceinline__ bool small_step(const float4* nodes4, const float4* t
         }
         return pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
     }
-    // statistics frames count the reference's node visits one level at a time
-    if (!STATS && two_level) {
-        if (inner_step2<STATS>(nodes4, stk, T.sp, R, h.best, T.first, T.count, c)) return true;
-    } else if (inner_step<STATS>(nodes4, stk, T.sp, R, h.best, T.first, T.count, c)) {
-        return true;
-    }
+    if (inner_step<STATS>(nodes4, stk, T.sp, R, h.best, T.first, T.count, c)) return true;
     return pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
 }
 
@@ -1437,7 +1350,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                                       const float4* tree, const float4* ltris, const float4* flat,
                                       const float4* spairs, uint32_t tune, const S& stk, uint32_t* scratch,
                                       const Ray& R, Hit& h, bool live, C& c, const float4* quads = nullptr,
-                                      const float4* units = nullptr, bool two_level = false) {
+                                      const float4* units = nullptr) {
     Trav T{0, 0, 0};
     bool active = live && trav_begin<STATS>(nodes4, R, h, T, c);
     // big-leaf screens (screen_leaf, MODE bit 5): split-step variants for scenes that have them
@@ -1486,7 +1399,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                 // exists to gather lanes per kind, which matters little when both groups are small)
                 if (!scr_on && mI && mL && nI + nL <= (uint32_t)RT_COMBINE_T) {
                     if (inner || leafs) {
-                        active = small_step<STATS>(nodes4, tris, spairs, stk, R, h, T, c, nullptr, two_level);
+                        active = small_step<STATS>(nodes4, tris, spairs, stk, R, h, T, c);
                         if (TIMING) c.lane_work++;
                     }
                 } else
@@ -1497,7 +1410,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                         if (TIMING) c.lane_work++;
                     }
                 } else if (inner) {
-                    active = small_step<STATS>(nodes4, tris, spairs, stk, R, h, T, c, nullptr, two_level);
+                    active = small_step<STATS>(nodes4, tris, spairs, stk, R, h, T, c);
                     if (TIMING) c.lane_work++;
                 }
 #ifdef RT_LANE_HIST
@@ -1523,7 +1436,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                 c.l_small += small;
             }
             if (small) {
-                active = small_step<STATS>(nodes4, tris, spairs, stk, R, h, T, c, nullptr, two_level);
+                active = small_step<STATS>(nodes4, tris, spairs, stk, R, h, T, c);
                 if (TIMING) c.lane_work++;
             }
             continue;

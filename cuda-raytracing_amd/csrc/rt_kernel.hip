@@ -836,13 +836,9 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     // reference-layout tracers keep the reference's
     const GPUBVHNode* const trav_nodes =
         (mir.nodes && (a.tune & (1u << 27)) == 0) ? (const GPUBVHNode*)mir.nodes : scene->gpu_bvh_nodes;
-    // two-level inner steps (rt_fast.h inner_step2): on the private array (R's children pair follows the
-    // pair of R) when every child box lies inside its parent's; RT_TUNE bit 24 turns them off (A/B)
-    const int two_level = (trav_nodes == (const GPUBVHNode*)mir.nodes && mir.nested && (a.tune & (1u << 24)) == 0) ? 1 : 0;
     auto trav = [&](const RenderArgs& x) {  // the arguments as they stand at launch, traversal nodes
         RenderArgs f = x;
         f.nodes = trav_nodes;
-        f.two_level = two_level;
         return f;
     };
     hipError_t e;
