@@ -529,6 +529,25 @@ def refine_lane_map(rt, render, rng, lm, cost, rounds, theta, dev, waves_per_sim
                  "s": round(time.perf_counter() - t0, 3)}
 
 
+def production_counts(t):
+    """The production kernel's own work on one frame, from its timing variant's counters (`t`: STAT_NAMES ->
+    value): where the wave cycles go (small steps / big-leaf rounds / the rest: shading, sky, RNG,
+    output), small-step wave iterations and their active lanes, and the big leaves' tests by twins
+    (mirror.h quads / units: unit triangles tested, twins decided from their partner's values, twins
+    tested).  frame0_counts beside it counts the reference's own work (statistics variant)."""
+    tot = max(1, t["cycles_total"])
+    out = {"cycles_frac": {"small": round(t["cycles_small"] / tot, 4), "big": round(t["cycles_big"] / tot, 4),
+                           "rest": round(1 - (t["cycles_small"] + t["cycles_big"]) / tot, 4)},
+           "wave_small_iters": t["wave_small_iters"], "lane_small": t["lane_small"],
+           "small_lanes_per_iter": round(t["lane_small"] / max(1, t["wave_small_iters"]), 2),
+           "rounds_coop": t["rounds_coop"], "rounds_shared": t["rounds_shared"], "coop_rays": t["coop_rays"],
+           "big_unit_tests": t["big_tests"], "twins_decided": t["twin_decided"], "twins_tested": t["twin_tests"],
+           "wave_big_iters": t["wave_big_iters"]}
+    if t["cycles_tree_cut"]:
+        out["cycles_frac"]["tree_walk"] = round(t["cycles_tree_cut"] / tot, 4)
+    return out
+
+
 def settle_occupancy(probe_occupancy, lane_slots, refine_occ, world, cdev):
     """The frames' occupancy with this rank's lane map (or None), and whether the map survives.
     probe_occupancy(map) -> (waves per SIMD, {wps: ms}) times each candidate and max-reduces over ranks,
@@ -631,11 +650,12 @@ def run(args):
 
     def render(i, cur, prev, **kw):
         ls = kw.pop("lane_slots", lane_slots)
+        tune = kw.pop("tune", args.tune)
         if sharded:
             rt.render(scene, None, prev, W, H, SPP, BOUNCES, i, rank, world, out_shard=cur, tile_list=tile_list,
-                      tune=args.tune, lane_slots=ls, **refill(kw))
+                      tune=tune, lane_slots=ls, **refill(kw))
         else:
-            rt.render(target, cur, prev, W, H, SPP, BOUNCES, i, tile_list=tile_list, tune=args.tune,
+            rt.render(target, cur, prev, W, H, SPP, BOUNCES, i, tile_list=tile_list, tune=tune,
                       lane_slots=ls, **refill(kw))
 
     occupancy = {"waves_per_simd": 0 if args.occupancy == "auto" else int(args.occupancy)}
@@ -721,12 +741,23 @@ def run(args):
 
     # --- exact traversal counts of one frame (stats kernel variant) on a copy of the RNG state
     rng_saved = rng.clone()
-    stats = torch.zeros(24, dtype=torch.int64, device=dev)
+    stats = torch.zeros(rt.STAT_COUNT, dtype=torch.int64, device=dev)
     render(0, bufs[0], bufs[1], stats=stats)
     torch.cuda.synchronize()
     rng.copy_(rng_saved)
     del rng_saved
     stats0 = stats.cpu().numpy().astype(np.uint64)
+    # --- the production kernel's own work on the same frame and launch shape: its timing variant (RT_TUNE
+    #     bit 8: per-wave phase clocks, small-step iterations and lane-steps, big-leaf tests by twins)
+    prod0 = None
+    if not args.foreign and args.tracer == "fast" and not args.refill:
+        rng_saved = rng.clone()
+        tst = torch.zeros(rt.STAT_COUNT, dtype=torch.int64, device=dev)
+        render(0, bufs[0], bufs[1], stats=tst, tune=args.tune | 256)
+        torch.cuda.synchronize()
+        rng.copy_(rng_saved)
+        del rng_saved
+        prod0 = production_counts(dict(zip(rt.STAT_NAMES, tst.cpu().numpy().astype(np.int64).tolist())))
     gpu = scene.gpu.contents
     bytes0 = algorithmic_bytes(stats0, gpu.sphere_count, pixels_rank)
     if args.foreign and rt.foreign_last_tracer(target) != 1:
@@ -854,6 +885,8 @@ def run(args):
                     pmc, err = pmc_pass(args, args.pmc_dir or td)
         roof = roofline(pmc, kern_avg_s, bytes_per_launch, err)
         roof["frame0_counts"] = {k: int(v) for k, v in zip(rt.STAT_NAMES, stats0) if k and int(v)}
+        if prod0:
+            roof["frame0_production"] = prod0
         result = {
             "metric": "Mrays/s + achieved HBM GB/s, Stanford bunny 1920x1080x8spp @1/2/4/8 GPU",
             "value": round(segs_total / elapsed / 1e6, 2),

@@ -32,7 +32,9 @@ TRACERS = {"fast": 0, "ref": 2, "flat": 4, "wavefront": 8}  # rt_render_params.f
 STAT_NAMES = ("segments", "nodes", "tri_tests", "tri_accepts", "sphere_accepts", "hits", "misses", "cycles_tree_cut",
               "wave_small_iters", "lane_small", "wave_big_tris", "lane_big_tris", "wave_segment_iters",
               "lane_segments", "tree_nodes", "tree_tri_tests", "cycles_small", "cycles_big", "cycles_total",
-              "rounds_coop", "rounds_shared", "coop_rays", "cycles_tree_clusters", "cycles_tree_tris")
+              "rounds_coop", "rounds_shared", "coop_rays", "cycles_tree_clusters", "cycles_tree_tris",
+              "big_tests", "twin_decided", "twin_tests", "wave_big_iters", None, None, None, None)
+STAT_COUNT = len(STAT_NAMES)  # RT_STAT_COUNT (include/rt_abi.h): per-wave records of RT_TUNE bit 11 follow
 SCENES = {"bunny": 0, "bunny4": 1, "plane1m": 2}
 
 REFERENCE_SPP = 5      # main_raytracing.cu:166-170 (Release)

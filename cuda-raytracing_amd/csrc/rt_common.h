@@ -81,6 +81,7 @@ struct Counters {
     unsigned long long cy_small = 0, cy_big = 0, r_coop = 0, r_shared = 0, coop_rays = 0, w_iter = 0;  // timing
     unsigned long long cy_tcl = 0, cy_ttri = 0, cy_tree = 0;  // timing: leaf-tree cluster / triangle rounds, whole walk
     uint32_t lane_work = 0;  // timing: this lane's own traversal steps (+3 per big leaf), rt_render_params.lane_cost
+    unsigned long long big_tests = 0, tw_test = 0, tw_dec = 0, big_iters = 0;  // timing: big-leaf work by twins
 };
 
 __device__ __forceinline__ rtm::f3 ld3(const float* p) { return rtm::f3{p[0], p[1], p[2]}; }

@@ -435,12 +435,18 @@ __device__ __forceinline__ void tri_offer(f3 o, f3 nd, f3 v0, f3 e1, f3 e2, uint
 // Quads (mirror.h): 7 float4 -- the pair layout (x5), the twin bounds (kd_a, kd_b, ke_a, ke_b; kd < 0:
 // no twin), and (pos_a | twin_a << 16, pos_b | twin_b << 16, twin face a, twin face b), read only on a
 // hit or a twin test.  One quad for one ray (the shared-leaf loop: scalar loads).
+template <bool TIMING, class C>
 __device__ __forceinline__ void quad_test(f3 o, f3 nd, const Pair& P, f4v bnd, ConstF4 q6, Hit& h, uint32_t& bpos,
-                                          bool& nan) {
+                                          bool& nan, C& c) {
     const PairEval E = pair_eval(o, nd, P);
     const bool oka = tri_ok(E.det.x, E.u.x, E.v.x, E.uv.x), okb = tri_ok(E.det.y, E.u.y, E.v.y, E.uv.y);
     const bool twa = bnd.x >= 0.0f && !twin_rejected(E.det.x, E.u.x, E.v.x, E.uv.x, E.dn.x, bnd.x, bnd.z);
     const bool twb = bnd.y >= 0.0f && !twin_rejected(E.det.y, E.u.y, E.v.y, E.uv.y, E.dn.y, bnd.y, bnd.w);
+    if (TIMING) {  // timing frames: the production kernel's own big-leaf work (RT_STAT_BIG_TESTS, ...)
+        c.big_tests += 2;
+        c.tw_test += (uint32_t)twa + (uint32_t)twb;
+        c.tw_dec += (uint32_t)(bnd.x >= 0.0f && !twa) + (uint32_t)(bnd.y >= 0.0f && !twb);
+    }
     if (oka || okb || twa || twb) {  // rare: a hit, or a twin too close to call
         const f4v W = *q6;
         const uint32_t wa = __float_as_uint(W.x), wb = __float_as_uint(W.y);
@@ -466,8 +472,9 @@ __device__ __forceinline__ void quad_test(f3 o, f3 nd, const Pair& P, f4v bnd, C
 // Units (mirror.h): 4 float4 -- a triangle record (v0, e1, e2, face) with (twin face, pos | twin << 16)
 // in its last two words, and (kd, ke, 0, 0); kd < 0: no twin.  One unit for one ray (cooperative
 // rounds: a lane per unit).
+template <bool TIMING, class C>
 __device__ __forceinline__ void unit_test(f3 o, f3 nd, float4 A, float4 B, float4 Cc, float4 D, Hit& h, uint32_t& bpos,
-                                          bool& nan) {
+                                          bool& nan, C& c) {
     const f3 v0 = rtm::mk(A.x, A.y, A.z), e1 = rtm::mk(A.w, B.x, B.y), e2 = rtm::mk(B.z, B.w, Cc.x);
     const f3 p = rtm::cross(nd, e2);
     const float det = rtm::dot(e1, p);
@@ -482,8 +489,9 @@ __device__ __forceinline__ void unit_test(f3 o, f3 nd, float4 A, float4 B, float
         offer(rtm::dot(e2, perp) * inv_det, w & 0xffffu, __float_as_uint(Cc.y), u * inv_det, v * inv_det, h, bpos, nan);
     }
     const float dn = (fabsf(dist.x) + fabsf(dist.y)) + fabsf(dist.z);
-    if (D.x >= 0.0f && !twin_rejected(det, u, v, uv, dn, D.x, D.y))
-        tri_offer(o, nd, v0, e2, e1, w >> 16, __float_as_uint(Cc.z), h, bpos, nan);
+    const bool tw = D.x >= 0.0f && !twin_rejected(det, u, v, uv, dn, D.x, D.y);
+    if (TIMING) c.big_tests++, c.tw_test += (uint32_t)tw, c.tw_dec += (uint32_t)(D.x >= 0.0f && !tw);
+    if (tw) tri_offer(o, nd, v0, e2, e1, w >> 16, __float_as_uint(Cc.z), h, bpos, nan);
 }
 
 // BVHRayHit's sequential loop over big leaf [f0, f0 + c0) for this lane (the NaN fallback).
@@ -573,8 +581,9 @@ __device__ __forceinline__ void coop_leaf(const float4* tris, const float4* pair
 // coop_leaf on a leaf's units (mirror.h): lane l tests units l, l + 64, ... for the one ray, keeping
 // its (t, position)-first candidate (offer); the wave's (t, position) arg-min is the sequential loop's
 // result.  A NaN distance, or a NaN entry distance, runs the sequential loop.
+template <bool TIMING, class C>
 __device__ __forceinline__ void coop_units(const float4* tris, const float4* un, uint32_t nu, unsigned long long big,
-                                           uint32_t f0, uint32_t c0, const Ray& R, Hit& h) {
+                                           uint32_t f0, uint32_t c0, const Ray& R, Hit& h, C& c) {
     const uint32_t lane = threadIdx.x & 63u;
     unsigned long long m = big;
     while (m) {
@@ -587,7 +596,8 @@ __device__ __forceinline__ void coop_units(const float4* tris, const float4* un,
         uint32_t bpos = NO_POS;
         bool nan = !(L.best == L.best);
         for (uint32_t q = lane; q < nu; q += 64u)
-            unit_test(rox, nd, un[4 * q], un[4 * q + 1], un[4 * q + 2], un[4 * q + 3], L, bpos, nan);
+            unit_test<TIMING>(rox, nd, un[4 * q], un[4 * q + 1], un[4 * q + 2], un[4 * q + 3], L, bpos, nan, c);
+        if (TIMING && lane == 0) c.big_iters += (nu + 63u) / 64u;
         if (__ballot(nan)) {
             if ((int)lane == r) leaf_sequential(tris, f0, c0, R.o, R.nd, h);
             continue;
@@ -1099,7 +1109,7 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
             // RT_TUNE bits 21-23: the cooperative side's weight in quarters (0 = 4, the default)
             const uint32_t cw = (tune >> 21) & 7u;
             if (nu && (tune & 1u) == 0 && k * (70u * ((nu + 63u) / 64u) + 70u) * (cw ? cw : 4u) < 4u * 95u * nq) {
-                coop_units(tris, units + 4 * (size_t)__float_as_uint(l3.z), nu, big, f0, c0, R, h);
+                coop_units<(MODE & 8) != 0>(tris, units + 4 * (size_t)__float_as_uint(l3.z), nu, big, f0, c0, R, h, c);
                 if (MODE & 8) c.r_coop++, c.coop_rays += k;
                 return waiting;
             }
@@ -1112,8 +1122,9 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
                 for (uint32_t q = 0; q < nq; q++, qs += 7) {
                     const Pair P = make_pair(qs[0], qs[1], qs[2], qs[3], qs[4]);
                     const f4v bnd = qs[5];
-                    if (waiting) quad_test(R.o, R.nd, P, bnd, qs + 6, h, bpos, nan);
+                    if (waiting) quad_test<(MODE & 8) != 0>(R.o, R.nd, P, bnd, qs + 6, h, bpos, nan, c);
                 }
+                if (MODE & 8) c.big_iters += nq;
                 if (waiting && nan) {  // the sequential loop from the entry distance (never taken for finite scenes)
                     h = h0;
                     leaf_sequential(tris, f0, c0, R.o, R.nd, h);

@@ -295,8 +295,12 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
             lane_max = o > lane_max ? o : lane_max;
         }
     unsigned long long lane_sum = c.l_small;  // the wave's lane-steps in small-step iterations (timing frame)
+    unsigned long long big_sum[3] = {c.big_tests, c.tw_dec, c.tw_test};  // per lane -> the wave's
     if ((MODE & 8) && a.stats)
-        for (int off = 32; off > 0; off >>= 1) lane_sum += __shfl_xor(lane_sum, off);
+        for (int off = 32; off > 0; off >>= 1) {
+            lane_sum += __shfl_xor(lane_sum, off);
+            for (int k = 0; k < 3; k++) big_sum[k] += __shfl_xor(big_sum[k], off);
+        }
     if ((MODE & 8) && a.stats && threadIdx.x == 0) {  // timing frame: per-wave phase clocks
         atomicAdd(a.stats + RT_STAT_CYCLES_SMALL, c.cy_small);
         atomicAdd(a.stats + RT_STAT_CYCLES_BIG, c.cy_big);
@@ -306,6 +310,10 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
         atomicAdd(a.stats + RT_STAT_COOP_RAYS, c.coop_rays);
         atomicAdd(a.stats + RT_STAT_WAVE_SMALL_ITERS, c.w_small);  // small-step wave iterations
         atomicAdd(a.stats + RT_STAT_LANE_SMALL, lane_sum);          // lane-steps in them
+        atomicAdd(a.stats + RT_STAT_BIG_TESTS, big_sum[0]);
+        atomicAdd(a.stats + RT_STAT_TWIN_DECIDED, big_sum[1]);
+        atomicAdd(a.stats + RT_STAT_TWIN_TESTS, big_sum[2]);
+        atomicAdd(a.stats + RT_STAT_WAVE_BIG_ITERS, c.big_iters);
         // cooperative leaf-tree walk (wave-level): rays, subtree + cluster tests, triangle rounds
         atomicAdd(a.stats + RT_STAT_TREE_NODES, c.ktest);
         atomicAdd(a.stats + RT_STAT_TREE_TRI_TESTS, c.ktri);

@@ -256,7 +256,12 @@ enum {
     RT_STAT_CYCLES_TREE_CUT = 7,    /* timing frames, cooperative leaf-tree walk: whole walk (all rounds) */
     RT_STAT_CYCLES_TREE_CLUSTERS = 22, /* ... cluster screening rounds */
     RT_STAT_CYCLES_TREE_TRIS = 23,  /* ... triangle rounds */
-    RT_STAT_COUNT = 24
+    /* timing frames: the production kernel's own big-leaf work with twin records (mirror.h quads / units) */
+    RT_STAT_BIG_TESTS = 24,         /* glm tests of a big leaf's unit triangles (quad halves, units), summed over rays */
+    RT_STAT_TWIN_DECIDED = 25,      /* twins rejected from their partner's values without a test (rt_fast.h twin_rejected) */
+    RT_STAT_TWIN_TESTS = 26,        /* twins tested themselves (too close to call, or a hit) */
+    RT_STAT_WAVE_BIG_ITERS = 27,    /* wave iterations of those tests (shared-leaf quads, cooperative unit chunks) */
+    RT_STAT_COUNT = 32
 };
 
 /* Render on `stream` (a hipStream_t, NULL = null stream).  Returns 0 or an error code.

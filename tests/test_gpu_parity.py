@@ -37,7 +37,7 @@ def gpu_render(rt, which, w, h, spp, bounces, frames=1, plane_n=None, seed=T.SEE
     rt.init_rng_states(rng, w, h, seed)
     s.upload(rng.data_ptr())
     a, b = rt.alloc_surface(w, h), rt.alloc_surface(w, h)
-    st = torch.zeros(24, dtype=torch.int64, device="cuda") if stats else None
+    st = torch.zeros(rt.STAT_COUNT, dtype=torch.int64, device="cuda") if stats else None
     outs = []
     for f in range(frames):
         cur, prev = (a, b) if f % 2 == 0 else (b, a)

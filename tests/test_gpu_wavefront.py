@@ -108,7 +108,7 @@ def test_wavefront_misuse_is_refused(rt):
     rt.init_rng_states(rng, w, h, T.SEED)
     s.upload(rng.data_ptr())
     out = rt.alloc_surface(w, h)
-    st = torch.zeros(24, dtype=torch.int64, device="cuda")
+    st = torch.zeros(rt.STAT_COUNT, dtype=torch.int64, device="cuda")
     with pytest.raises(RuntimeError, match="wavefront"):
         rt.render(s, out, out, w, h, 1, 1, 0, stats=st, tracer="wavefront")
     with pytest.raises(RuntimeError, match="spp x bounces"):

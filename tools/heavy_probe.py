@@ -50,13 +50,13 @@ def breakdown(rt, scene, W, H, SPP, BOUNCES, tiles):
     for name, tune in [("timing", 256 + 2048), ("stats", 0)]:
         rt.init_rng_tiles(rng, W, H, mine, bench.SEED)
         scene.upload(rng.data_ptr())
-        st = torch.zeros(24 + 8 * len(tiles) * 4, dtype=torch.int64, device="cuda")
+        st = torch.zeros(rt.STAT_COUNT + 8 * len(tiles) * 4, dtype=torch.int64, device="cuda")
         rt.render(scene, None, None, W, H, SPP, BOUNCES, 0, 0, 1, out_shard=out, tile_list=mine, stats=st, tune=tune)
         torch.cuda.synchronize()
         v = st.cpu().numpy()
         res[name] = [int(x) for x in v[:24]]
         if name == "timing":
-            res["waves"] = [[int(x) for x in r] for r in v[24:].reshape(-1, 8)]
+            res["waves"] = [[int(x) for x in r] for r in v[rt.STAT_COUNT:].reshape(-1, 8)]
     return res
 
 

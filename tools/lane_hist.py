@@ -27,7 +27,7 @@ rt.init_rng_states(rng, W, H, bench.SEED)
 scene.upload(rng.data_ptr())
 a, b = rt.alloc_surface(W, H), rt.alloc_surface(W, H)
 for wps in (0, 7):
-    st = torch.zeros(24, dtype=torch.int64, device="cuda")
+    st = torch.zeros(rt.STAT_COUNT, dtype=torch.int64, device="cuda")
     rt.render(scene, a, b, W, H, SPP, BOUNCES, 0, stats=st, tune=256, waves_per_simd=wps)
     torch.cuda.synchronize()
     v = [int(x) for x in st.cpu().numpy()]

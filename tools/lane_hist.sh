@@ -8,7 +8,7 @@ cd "$(dirname "$0")/.."
 B=cuda-raytracing_amd/build; V=cuda-raytracing_amd/variants
 mkdir -p "$V" /tmp/rtvar
 /opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
-  -fhip-fp32-correctly-rounded-divide-sqrt -munsafe-fp-atomics -fno-slp-vectorize -mllvm -structurizecfg-skip-uniform-regions=1 \
+  -fhip-fp32-correctly-rounded-divide-sqrt -munsafe-fp-atomics -fno-slp-vectorize -mllvm -structurizecfg-skip-uniform-regions=1 -mllvm -amdgpu-remove-redundant-endcf=0 \
   -DRT_LANE_HIST=1 -I include -I cuda-raytracing_amd/csrc -c cuda-raytracing_amd/csrc/rt_fast_timing.hip -o /tmp/rtvar/timing_hist.o
 objs=""
 for o in $B/*.o; do

@@ -25,7 +25,7 @@ rng = rt.alloc_rng(W * H)
 rt.init_rng_states(rng, W, H, bench.SEED)
 scene.upload(rng.data_ptr())
 a, b = rt.alloc_surface(W, H), rt.alloc_surface(W, H)
-st = torch.zeros(24, dtype=torch.int64, device="cuda")
+st = torch.zeros(rt.STAT_COUNT, dtype=torch.int64, device="cuda")
 wps = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 extra = int(sys.argv[3], 0) if len(sys.argv) > 3 else 0
 rt.render(scene, a, b, W, H, SPP, BOUNCES, 0, stats=st, tune=256 | ({6: 2, 7: 3}.get(wps, 0) << 9) | extra)

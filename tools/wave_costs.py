@@ -28,14 +28,14 @@ rt.init_rng_states(rng, W, H, bench.SEED, 0, N)
 scene.upload(rng.data_ptr())
 a, b = rt.alloc_surface(W, H), rt.alloc_surface(W, H)
 shard = torch.zeros((tiles * 256, 4), dtype=torch.float32, device="cuda")
-st = torch.zeros(24 + 8 * tiles * 4, dtype=torch.int64, device="cuda")
+st = torch.zeros(rt.STAT_COUNT + 8 * tiles * 4, dtype=torch.int64, device="cuda")
 if N > 1:
     rt.render(scene, None, None, W, H, SPP, BOUNCES, 0, 0, N, out_shard=shard, stats=st, tune=256 + 2048)
 else:
     rt.render(scene, a, b, W, H, SPP, BOUNCES, 0, stats=st, tune=256 + 2048)
 torch.cuda.synchronize()
 v = st.cpu().numpy()
-t = v[24:].reshape(-1, 8)
+t = v[rt.STAT_COUNT:].reshape(-1, 8)
 dur = (t[:, 1] - t[:, 0]).astype(np.float64)
 t0 = t[:, 0].min()
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)

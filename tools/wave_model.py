@@ -196,12 +196,12 @@ def measure(args):
             out[f"n{n}_r{r}_full_per_frame"] = full_per.astype(np.float32)
             # one timing frame (RT_TUNE 256 + 2048) at the same occupancy: every wave's start and end on
             # the 100 MHz device clock, indexed by hardware workgroup (dispatch order)
-            st = torch.zeros(24 + 8 * waves, dtype=torch.int64, device="cuda")
+            st = torch.zeros(rt.STAT_COUNT + 8 * waves, dtype=torch.int64, device="cuda")
             rt.render(scene, None, None, W, H, SPP, BOUNCES, 0, 0, 1, out_shard=buf, tile_list=mine, lane_slots=lm,
                       stats=st, tune=256 | 2048, waves_per_simd=args.wps)
             torch.cuda.synchronize()
             rng.copy_(saved)
-            rec = st[24:].view(-1, 8).cpu().numpy()
+            rec = st[rt.STAT_COUNT:].view(-1, 8).cpu().numpy()
             t0 = rec[:, 0].min()
             out[f"n{n}_r{r}_start"] = (rec[:, 0] - t0) / CLOCK_HZ * 1e3
             out[f"n{n}_r{r}_end"] = (rec[:, 1] - t0) / CLOCK_HZ * 1e3

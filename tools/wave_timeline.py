@@ -61,7 +61,7 @@ def main():
     res = {}
     for label, tune in (("production", 0), ("timing", 256 + 2048)):
         rt.init_rng_tiles(rng, W, H, mine, bench.SEED)
-        st = torch.zeros(24 + 8 * waves, dtype=torch.int64, device="cuda")
+        st = torch.zeros(rt.STAT_COUNT + 8 * waves, dtype=torch.int64, device="cuda")
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         rt.render(scene, None, None, W, H, SPP, BOUNCES, 0, out_shard=out, tile_list=mine, lane_slots=lmd,
@@ -69,7 +69,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         res[label] = e0.elapsed_time(e1)
-    t = st.cpu().numpy()[24:].reshape(-1, 8)
+    t = st.cpu().numpy()[rt.STAT_COUNT:].reshape(-1, 8)
     start, end = t[:, 0].astype(np.float64), t[:, 1].astype(np.float64)
     t0 = start.min()
     start, end = (start - t0) / 1e5, (end - t0) / 1e5  # ms
