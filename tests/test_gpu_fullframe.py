@@ -240,3 +240,35 @@ def test_every_occupancy_build_equals_oracle(rt, which, mirror, wps):
         rt.set_build_options()
     bad = int((got.view(np.uint32) != want.view(np.uint32)).any(-1).sum())
     assert bad == 0, f"{which} mirror={mirror} at {wps} waves per SIMD: {bad} pixels differ from the oracle"
+
+
+def _row_hashes(a):
+    import hashlib
+    return [hashlib.sha256(np.ascontiguousarray(r).tobytes()).hexdigest()[:16] for r in a]
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg4"])
+def test_full_frame_matches_oracle_fixture(rt, cfg):
+    """The whole frame of configs 2, 3 (3840x2160 64 spp) and 4 (the 4-bunny scene) against the CPU oracle's
+    own full frame: tools/make_fullframe_golden.py rendered each once with oracle/rt_oracle.c (minutes of CPU
+    per config, too long for this box) and tests/golden/fullframe_oracle.json keeps a SHA-256 of every row of
+    the float32 frame and of the final RNG states (data only).  The production kernel's frame (default launch:
+    plain tile order, 5 waves per SIMD) must hash equal row for row -- bit-exact, every pixel and every final
+    RNG state; a mismatch names the first rows."""
+    db = json.load(open(os.path.join(T.GOLDEN, "fullframe_oracle.json")))
+    if cfg not in db:
+        pytest.skip(f"no oracle fixture for {cfg} (tools/make_fullframe_golden.py {cfg})")
+    g = db[cfg]
+    img, st = render_gpu(rt, g["scene"], g["width"], g["height"], g["spp"], g["bounces"])
+    img = img.reshape(g["height"], g["width"], 4)
+    rows = _row_hashes(img)
+    rng_rows = _row_hashes(st.reshape(g["height"], g["width"], 6))
+    bad = [y for y, (a, b) in enumerate(zip(rows, g["rows"])) if a != b]
+    bad_rng = [y for y, (a, b) in enumerate(zip(rng_rows, g["rng_rows"])) if a != b]
+    with open(SUMMARY, "a") as fh:
+        fh.write(json.dumps({"test": f"{cfg} full frame vs the oracle's full frame (row hashes, tests/golden/fullframe_oracle.json)",
+                             "values": int(img.size), "rows": len(rows), "differing_rows": len(bad),
+                             "differing_rng_rows": len(bad_rng), "nan_values": int(np.isnan(img).sum()),
+                             "oracle_nan_values": g["nan_values"]}) + "\n")
+    assert not bad and not bad_rng, f"{cfg}: {len(bad)} frame rows / {len(bad_rng)} RNG rows differ, first {bad[:5]} {bad_rng[:5]}"
+    assert int(np.isnan(img).sum()) == g["nan_values"]

@@ -128,6 +128,50 @@ def simulate(alone_ms, k0, slots, order=None):
     return finish, simd_of
 
 
+GDEV = 0.0  # device-load term (--c-dev): rate / ((1 + GDEV D) / (1 + GDEV / slots)), D = resident / (SIMDS x slots)
+
+
+def simulate_dt(alone_ms, k0, slots, order=None, dt=0.004):
+    """simulate() as a time-stepped, vectorised processor-sharing simulation (steps of `dt` ms), which
+    also carries the device-load term: a wave on a SIMD with k resident waves progresses at
+    1 / max(1, k / k0), divided by (1 + GDEV D) / (1 + GDEV / slots) where D is the fraction of the
+    device's wave slots in use -- the alone measurement (one wave per SIMD) is the reference point.
+    Same placement as simulate(): wave i of the dispatch order to SIMD i mod SIMDS, `slots` deep, a
+    freed slot takes the next wave.  Returns the finish time of every wave (in `order`'s numbering)."""
+    n = len(alone_ms)
+    order = np.arange(n) if order is None else np.asarray(order)
+    rem = np.asarray(alone_ms, dtype=np.float64)[order].copy()  # dispatch order
+    slot = np.full((SIMDS, slots), -1, dtype=np.int64)
+    m = min(n, slots * SIMDS)
+    i = np.arange(m)
+    slot[i % SIMDS, i // SIMDS] = i
+    nxt, t = m, 0.0
+    fin = np.zeros(n)
+    ref = 1.0 + GDEV / slots
+    while True:
+        occ = slot >= 0
+        k = occ.sum(1)
+        tot = int(k.sum())
+        if tot == 0:
+            break
+        r = 1.0 / (np.maximum(1.0, k / k0) * (1.0 + GDEV * tot / (SIMDS * slots)) / ref)
+        ids = slot[occ]
+        rem[ids] -= dt * np.broadcast_to(r[:, None], slot.shape)[occ]
+        t += dt
+        done = ids[rem[ids] <= 0]
+        if done.size:
+            fin[done] = t
+            pos = np.argwhere(np.isin(slot, done))
+            slot[pos[:, 0], pos[:, 1]] = -1
+            take = min(len(pos), n - nxt)
+            if take > 0:
+                slot[pos[:take, 0], pos[:take, 1]] = np.arange(nxt, nxt + take)
+                nxt += take
+    out = np.zeros(n)
+    out[order] = fin
+    return out
+
+
 def xcd_order(waves):
     """Logical wave index of hardware workgroup g (rt_fast_body.h xcd_block, runs of 32 per XCD)."""
     S = 32
@@ -222,40 +266,54 @@ def measure(args):
 
 
 def fit_k0(args):
-    """The one free constant, k0, fitted to the measured shard times (least squares in log space over
-    the slowest rank of every N), beside the microbenchmark's 8.2 / 1.8."""
+    """The free constants -- k0, and the device-load term GDEV with --fit-dev -- fitted to the measured
+    shard times of the N in --fit-ns only (least squares in log space over the slowest rank of each N),
+    beside the microbenchmark's k0 = 8.2 / 1.8; the other N are then out of sample."""
+    global GDEV
+    fit_ns = {int(x) for x in args.fit_ns.split(",")}
     best = None
-    for k0 in np.arange(2.0, 8.01, 0.25):
-        a = argparse.Namespace(**vars(args))
-        a.k0 = float(k0)
-        s = model(a, quiet=True)
-        err = sum(np.log(v["model_ms"] / v["measured_ms"]) ** 2 for v in s.values())
-        if best is None or err < best[0]:
-            best = (err, float(k0))
+    for g in ((0.0, 0.25, 0.5, 1.0, 1.5, 2.0) if args.fit_dev else (GDEV,)):
+        GDEV = g
+        for k0 in np.arange(3.5, 7.01, 0.25):
+            a = argparse.Namespace(**vars(args))
+            a.k0 = float(k0)
+            s = model(a, quiet=True, ns=fit_ns)
+            err = sum(np.log(v["model_ms"] / v["measured_ms"]) ** 2 for v in s.values())
+            if best is None or err < best[0]:
+                best = (err, float(k0), g)
+    GDEV = best[2]
     return best[1]
 
 
-def model(args, quiet=False):
+def model(args, quiet=False, ns=None):
     d = np.load(args.model)
     keys = sorted({k.rsplit("_", 1)[0] for k in d.files if k.endswith("_meta")})
     rows = []
     for key in keys:
         meta = d[key + "_meta"]
         shard_ms, n, r, waves = float(meta[0]), int(meta[3]), int(meta[4]), int(meta[5])
+        if ns is not None and n not in ns:
+            continue
         alone, full, pix = d[key + "_alone"], d[key + "_full"], d[key + "_pixels"]
         lb = xcd_order(waves)  # hardware dispatch order g -> logical wave lb
         if key + "_alone_per_frame" in d.files:
             # frame by frame: each frame's own waves (the longest wave differs from frame to frame, and
             # a strong-scaled frame ends with its longest), against that frame's measured time
             per = d[key + "_alone_per_frame"].astype(np.float64)
-            preds = [float(simulate(a, args.k0, args.slots, order=lb)[0].max()) for a in per]
-            shard_ms = float(d[key + "_frames_ms"].mean())
+            preds = [float(simulate_dt(a, args.k0, args.slots, order=lb).max()) for a in per[: (1 if quiet else len(per))]]
+            shard_ms = float(d[key + "_frames_ms"][: len(preds)].mean())
+            if quiet:
+                rows.append({"n": n, "rank": r, "measured_ms": shard_ms, "model_ms": float(np.mean(preds))})
+                continue
             fin, simd = simulate(per[int(np.argmax(preds))], args.k0, args.slots, order=lb)
             alone = per[int(np.argmax(preds))]
             pred = float(np.mean(preds))
         else:
             fin, simd = simulate(alone, args.k0, args.slots, order=lb)
-            pred = float(fin.max())
+            pred = float(simulate_dt(alone, args.k0, args.slots, order=lb).max())
+            if quiet:
+                rows.append({"n": n, "rank": r, "measured_ms": shard_ms, "model_ms": pred})
+                continue
         crit = int(simd[int(np.argmax(fin))])
         on = np.flatnonzero(simd == crit)
         rows.append({"n": n, "rank": r, "waves": waves, "measured_ms": round(shard_ms, 3), "model_ms": round(pred, 3),
@@ -276,14 +334,16 @@ def model(args, quiet=False):
         return summary
     for row in rows:
         print(json.dumps(row))
-    print(json.dumps({"k0": args.k0, "slots": args.slots, "per_n_slowest_rank": summary}))
+    print(json.dumps({"k0": args.k0, "device_load_term": GDEV, "slots": args.slots,
+                      "fitted_on_n": args.fit_ns if args.fit else None, "per_n_slowest_rank": summary}))
     return summary
 
 
 def whatif(args):
-    """The model's answer to the two levers, on the slowest rank of every N: every chain shorter by 10 /
-    20 / 30 % (a faster kernel), or the waves above a threshold split in two halves of 0.79x their
-    alone time each (the measured cost of halving a wave's pixels), dispatched longest first."""
+    """The model's answer to the two levers, on the slowest rank of every N (its first measured frame, with
+    the run's k0 and device-load term): every chain shorter by 10 / 20 / 30 % (a faster kernel), or the
+    waves above a threshold split in two halves of 0.79x their alone time each (the measured cost of
+    halving a wave's pixels), dispatched longest first."""
     d = np.load(args.model)
     keys = sorted({k.rsplit("_", 1)[0] for k in d.files if k.endswith("_meta")})
     worst = {}
@@ -293,16 +353,19 @@ def whatif(args):
         if n not in worst or meta[0] > d[worst[n] + "_meta"][0]:
             worst[n] = key
     for n, key in sorted(worst.items()):
-        a = d[key + "_alone"]
-        out = {"n": n, "rank": int(d[key + "_meta"][4]), "measured_ms": round(float(d[key + "_meta"][0]), 3),
-               "model_ms": round(float(simulate(a, args.k0, args.slots, order=xcd_order(len(a)))[0].max()), 3)}
+        per = key + "_alone_per_frame"
+        a = d[per][0].astype(np.float64) if per in d.files else d[key + "_alone"].astype(np.float64)
+        meas = float(d[key + "_frames_ms"][0]) if per in d.files else float(d[key + "_meta"][0])
+        lb = xcd_order(len(a))
+        sim = lambda x, o=lb: round(float(simulate_dt(x, args.k0, args.slots, order=o).max()), 3)
+        out = {"n": n, "rank": int(d[key + "_meta"][4]), "measured_ms": round(meas, 3), "model_ms": sim(a)}
         for f in (0.9, 0.8, 0.7):
-            out[f"chain_x{f}"] = round(float(simulate(a * f, args.k0, args.slots, order=xcd_order(len(a)))[0].max()), 3)
+            out[f"chain_x{f}"] = sim(a * f)
         for thr in (3.0, 2.5, 2.0):
             big = a > thr
             b = np.concatenate([a[~big], np.repeat(a[big] * 0.79, 2)])
             b = b[np.argsort(-b)]
-            out[f"split_above_{thr}ms"] = [round(float(simulate(b, args.k0, args.slots)[0].max()), 3), int(b.size)]
+            out[f"split_above_{thr}ms"] = [sim(b, None), int(b.size)]
         print(json.dumps(out))
 
 
@@ -319,13 +382,18 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "wave_model.npz"))
     ap.add_argument("--k0", type=float, default=8.2 / 1.8)
     ap.add_argument("--slots", type=int, default=7)
-    ap.add_argument("--fit", action="store_true", help="fit k0 to the measured shard times instead")
+    ap.add_argument("--fit", action="store_true", help="fit k0 (and the device-load term with --fit-dev) to the "
+                    "measured shard times of --fit-ns instead; the other N are out of sample")
+    ap.add_argument("--fit-ns", default="1,2,4")
+    ap.add_argument("--fit-dev", action="store_true")
+    ap.add_argument("--c-dev", type=float, default=0.0, help="device-load term (simulate_dt)")
     ap.add_argument("--dispatch", default="rr", choices=["rr", "fill", "xcd"], help="initial wave placement")
     ap.add_argument("--c0", type=float, default=0.0, help="CU-level saturation in waves per CU (0 = off)")
     ap.add_argument("--whatif", action="store_true", help="also price the two levers (shorter chains, split waves)")
     args = ap.parse_args()
-    global DISPATCH, C0
+    global DISPATCH, C0, GDEV
     DISPATCH = args.dispatch
+    GDEV = args.c_dev
     C0 = args.c0 if args.c0 > 0 else 1e9
     if args.measure:
         measure(args)
