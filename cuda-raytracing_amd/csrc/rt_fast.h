@@ -137,6 +137,17 @@ __device__ __forceinline__ void test_triangle(const Ray& R, float4 A, float4 B, 
 }
 
 typedef float f4v __attribute__((ext_vector_type(4)));
+
+// float4 `i` of `base` through a 32-bit byte offset (i < 2^28): the load then takes the SGPR base + VGPR
+// offset form (global_load ... v_off, s[base]) instead of a 64-bit address computed per lane
+// (v_lshl_add_u64 / v_mad_u64_u32 on every node, pair and record load of the traversal loop).
+__device__ __forceinline__ float4 ldo(const float4* base, uint32_t i) {
+#if defined(RT_ADDR64)
+    return base[i];
+#else
+    return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + (i << 4));
+#endif
+}
 typedef const __attribute__((address_space(4))) f4v* ConstF4;  // scalar-load (SMEM) view
 __device__ __forceinline__ float4 ldc(ConstF4 p, uint32_t i) {
     const f4v v = p[i];
@@ -168,7 +179,7 @@ __device__ __forceinline__ bool pop(const float4* nodes4, const S& stk, int& sp,
     while (sp > 0) {
         sp--;
         const uint32_t idx = stk.get(sp);
-        const float4 lo = nodes4[2 * idx], hi = nodes4[2 * idx + 1];
+        const float4 lo = ldo(nodes4, 2 * idx), hi = ldo(nodes4, 2 * idx + 1);
         int cl = UNSURE;
         float te, tx;
         if (R.fast) {
@@ -196,8 +207,8 @@ __device__ __forceinline__ bool pop(const float4* nodes4, const S& stk, int& sp,
 template <bool STATS, class S, class C>
 __device__ __forceinline__ bool inner_step(const float4* nodes4, const S& stk, int& sp, const Ray& R, float best,
                                            uint32_t& first, uint32_t& count, C& c) {
-    const float4 l0 = nodes4[2 * first], l1 = nodes4[2 * first + 1];
-    const float4 r0 = nodes4[2 * first + 2], r1 = nodes4[2 * first + 3];
+    const float4 l0 = ldo(nodes4, 2 * first), l1 = ldo(nodes4, 2 * first + 1);
+    const float4 r0 = ldo(nodes4, 2 * first + 2), r1 = ldo(nodes4, 2 * first + 3);
     if (STATS) c.node += 2;
     float tl = 0.0f, tlx = 0.0f, tr = 0.0f, trx = 0.0f;
     int okl = UNSURE, okr = UNSURE, rlt = UNSURE;
@@ -309,7 +320,11 @@ __device__ __forceinline__ Pair ld_pair_scalar(ConstF4 base, uint32_t p) {
     return make_pair(base[5 * p], base[5 * p + 1], base[5 * p + 2], base[5 * p + 3], base[5 * p + 4]);
 }
 __device__ __forceinline__ Pair ld_pair(const float4* base, uint32_t p) {
+#if defined(RT_ADDR64)
     const f4v* q = reinterpret_cast<const f4v*>(base) + 5 * (size_t)p;
+#else
+    const f4v* q = reinterpret_cast<const f4v*>(reinterpret_cast<const char*>(base) + p * 80u);  // 32-bit offset
+#endif
     return make_pair(q[0], q[1], q[2], q[3], q[4]);
 }
 
