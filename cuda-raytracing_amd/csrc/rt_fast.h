@@ -161,13 +161,27 @@ __device__ __forceinline__ float4 ldc(ConstF4 p, uint32_t i) {
 template <int SL>
 struct Stack {
     static constexpr int LDS_ENTRIES = SL;
-    uint32_t* lds;  // this lane's entry 0 (entry i at lds[i * WAVE])
-    uint32_t* ovf;  // entries SL, SL + 1, ...
-    __device__ __forceinline__ void put(int i, uint32_t v) const {
-        if (i < SL) lds[i * WAVE] = v;
-        else ovf[i - SL] = v;
+    // A lane's stack pointer is ENCODED as the byte offset of its next entry from lane 0's entry 0:
+    // sp = 4 * lane + 256 * depth (entry i of lane l at lds0[l + i * WAVE]).  The LDS address of an entry is
+    // then lds0 + sp, one wave-uniform base and the pointer the lane already holds: no per-lane column
+    // address to keep live beside it (the 7-wave build spilled that address and reloaded it on every pop).
+    uint32_t* lds0;  // lane 0's entry 0 (wave-uniform)
+    uint32_t* ovf;   // this lane's entries SL, SL + 1, ...
+    static __device__ __forceinline__ int depth(int sp) { return sp >> 8; }
+    static __device__ __forceinline__ int empty(int lane) { return 4 * lane; }  // sp of an empty stack
+    static constexpr int STEP = 4 * WAVE;                                         // sp per entry
+    __device__ __forceinline__ uint32_t* at(int sp) const {
+        return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(lds0) + sp);
     }
-    __device__ __forceinline__ uint32_t get(int i) const { return i < SL ? lds[i * WAVE] : ovf[i - SL]; }
+    // the overflow entries as a rare branch of their own
+    __device__ __forceinline__ void put(int sp, uint32_t v) const {
+        if (__builtin_expect(depth(sp) >= SL, 0)) ovf[depth(sp) - SL] = v;
+        else *at(sp) = v;
+    }
+    __device__ __forceinline__ uint32_t get(int sp) const {
+        if (__builtin_expect(depth(sp) >= SL, 0)) return ovf[depth(sp) - SL];
+        return *at(sp);
+    }
 };
 
 // Pop stack entries until one passes `tmin < closest` (the reference's pop-time test).  An
@@ -176,8 +190,8 @@ struct Stack {
 template <class S>
 __device__ __forceinline__ bool pop(const float4* nodes4, const S& stk, int& sp, const Ray& R, float best,
                                     uint32_t& first, uint32_t& count) {
-    while (sp > 0) {
-        sp--;
+    while (sp >= S::STEP) {  // depth > 0 (sp = 4 * lane + 256 * depth)
+        sp -= S::STEP;
         const uint32_t idx = stk.get(sp);
         const float4 lo = ldo(nodes4, 2 * idx), hi = ldo(nodes4, 2 * idx + 1);
         int cl = UNSURE;
@@ -231,7 +245,7 @@ __device__ __forceinline__ bool inner_step(const float4* nodes4, const S& stk, i
     if (rlt == YES) {
         if (okl == YES) {
             stk.put(sp, first);
-            sp++;
+            sp += S::STEP;
         }
         first = __float_as_uint(r1.z), count = __float_as_uint(r1.w);
         return true;
@@ -831,7 +845,7 @@ __device__ __forceinline__ void tree_leaf(const float4* tris, const float4* tree
 // Traversal state of one lane between steps: the node (or leaf) it is at and its stack depth.
 struct Trav {
     uint32_t first, count;
-    int sp;  // stack depth; bit SCREENED: at a big leaf whose screen has run (waiting for the round)
+    int sp;  // stack pointer, encoded (Stack: 4 * lane + 256 * depth); bit SCREENED: at a big leaf whose screen has run
 };
 // Trav::sp flag (screen variants): the lane's big leaf has been screened and it waits for the wave's
 // big-leaf round.  Kept in the depth word rather than in a bool of its own (a per-lane bool lives in a
@@ -1009,7 +1023,7 @@ __device__ __forceinline__ bool trav_begin(const float4* nodes4, const Ray& R, c
     if (STATS) c.node++;
     float tmin, tmax;
     slab_exact(R, lo, hi, &tmin, &tmax);
-    T.first = __float_as_uint(hi.z), T.count = __float_as_uint(hi.w), T.sp = 0;
+    T.first = __float_as_uint(hi.z), T.count = __float_as_uint(hi.w), T.sp = (int)(threadIdx.x & 63u) * 4;  // empty
     return tmax >= tmin && tmin < h.best && tmax > 0.0f;
 }
 
@@ -1216,8 +1230,8 @@ template <int SL>
 __device__ __forceinline__ void lone_traverse(const float4* nodes4, const float4* tris, const Stack<SL>& stk, int r,
                                               const Ray& R, Hit& h, Trav& T, bool& active) {
     const int lane = (int)(threadIdx.x & 63u);
-    uint32_t* const col = stk.lds - lane + r;  // lane r's LDS stack column
-    int sp = (int)bcastu((uint32_t)T.sp, r);
+    uint32_t* const col = stk.lds0 + r;  // lane r's LDS stack column
+    int sp = Stack<SL>::depth((int)bcastu((uint32_t)T.sp, r));  // lane r's depth
     uint32_t cf = bcastu(T.first, r), cc = bcastu(T.count, r);
     Ray U;  // the lone ray, wave-uniform
     U.o = bcast3(R.o, r), U.d = bcast3(R.d, r), U.nd = bcast3(R.nd, r), U.r = bcast3(R.r, r);
@@ -1352,7 +1366,7 @@ __device__ __forceinline__ void lone_traverse(const float4* nodes4, const float4
     }
     // back to lane r: its traversal state, hit, and (when it stops at a big leaf) its stack
     if (lane == r) {
-        T.first = cf, T.count = cc, T.sp = sp;
+        T.first = cf, T.count = cc, T.sp = Stack<SL>::empty(r) + sp * Stack<SL>::STEP;
         h.best = best, h.kind = kind, h.id = id, h.bx = bx, h.by = by;
         active = !done;
     }
@@ -1360,7 +1374,7 @@ __device__ __forceinline__ void lone_traverse(const float4* nodes4, const float4
         if (lane < sp && lane < SL) col[lane * WAVE] = e_idx;
         for (int j = SL; j < sp; j++) {
             const uint32_t v = bcastu(e_idx, j);
-            if (lane == r) stk.put(j, v);
+            if (lane == r) stk.put(Stack<SL>::empty(r) + j * Stack<SL>::STEP, v);
         }
     }
 }
@@ -1401,7 +1415,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                     // screen a big leaf first takes an ordinary step
                     if (nI + nL == 1 && (tune & (1u << 26)) == 0) {
                         const int r = __ffsll((long long)(mI | mL)) - 1;
-                        if (__builtin_amdgcn_readlane(T.sp, r) <= S::LDS_ENTRIES &&
+                        if (S::depth(__builtin_amdgcn_readlane(T.sp, r)) <= S::LDS_ENTRIES &&
                             (!scr_on || (uint32_t)__builtin_amdgcn_readlane((int)T.count, r) <= (uint32_t)BIG)) {
 #ifdef RT_LANE_HIST  // diagnostic build (tools/lane_hist.sh): wave cycles of the lone-lane tails
                             const unsigned long long tl0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;

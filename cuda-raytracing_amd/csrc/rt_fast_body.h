@@ -366,7 +366,7 @@ __global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
     __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
     __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
-    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds + threadIdx.x, ovf}, scratch_lds);
+    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds, ovf}, scratch_lds);
 }
 template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(5))) void render_fast_kernel_w5(RenderArgs a) {
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(5))) void 
     __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
     __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
-    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds + threadIdx.x, ovf}, scratch_lds);
+    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds, ovf}, scratch_lds);
 }
 template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(6))) void render_fast_kernel_w6(RenderArgs a) {
@@ -382,7 +382,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(6))) void 
     __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
     __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
-    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds + threadIdx.x, ovf}, scratch_lds);
+    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds, ovf}, scratch_lds);
 }
 template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(7))) void render_fast_kernel_w7(RenderArgs a) {
@@ -390,7 +390,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(7))) void 
     __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
     __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
-    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds + threadIdx.x, ovf}, scratch_lds);
+    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds, ovf}, scratch_lds);
 }
 
 // Waves of `kernel` the device holds at once (refill launches size their grid to it).

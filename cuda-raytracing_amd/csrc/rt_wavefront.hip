@@ -255,7 +255,7 @@ __device__ __forceinline__ void wf_trace_body(const RenderArgs& a, const WfBuf& 
     __shared__ uint32_t stack_lds[SL * WAVE];
     __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
-    const rtfast::Stack<SL> stk{stack_lds + threadIdx.x, ovf};
+    const rtfast::Stack<SL> stk{stack_lds, ovf};
     const float4* nodes4 = reinterpret_cast<const float4*>(a.nodes);
     const float4* tris = reinterpret_cast<const float4*>(a.tris);
     const uint32_t tv = (a.tune >> 20) & 7u, refill_min = tv ? 4u * tv : 4u;
@@ -290,7 +290,7 @@ __device__ __forceinline__ void wf_trace_body(const RenderArgs& a, const WfBuf& 
                         const rtm::f3 ro = rtm::mk(q0.x, q0.y, q0.z), rd = rtm::mk(q0.w, q1.x, q1.y);
                         R = rtfast::make_ray(ro, rd, rtm::normalize(rd), a.scene_fast != 0);
                         h = unpack_hit(make_float4(q1.z, q1.w, 0.0f, 0.0f));
-                        T.first = root_first, T.count = root_count, T.sp = 0;
+                        T.first = root_first, T.count = root_count, T.sp = rtfast::Stack<SL>::empty((int)(threadIdx.x & 63u));
                         active = true;
                         has = true;
                     }
@@ -312,7 +312,7 @@ __device__ __forceinline__ void wf_trace_body(const RenderArgs& a, const WfBuf& 
             const uint32_t nI = (uint32_t)__popcll(mI), nL = (uint32_t)__popcll(mL);
             if (exhausted && nI + nL == 1 && (a.tune & (1u << 26)) == 0) {
                 const int r = __ffsll((long long)(mI | mL)) - 1;
-                if (__builtin_amdgcn_readlane(T.sp, r) <= rtfast::Stack<SL>::LDS_ENTRIES) {
+                if (rtfast::Stack<SL>::depth(__builtin_amdgcn_readlane(T.sp, r)) <= rtfast::Stack<SL>::LDS_ENTRIES) {
                     rtfast::lone_traverse(nodes4, tris, stk, r, R, h, T, active);
                     continue;
                 }

@@ -243,7 +243,13 @@ def test_every_occupancy_build_equals_oracle(rt, which, mirror, wps):
 
 
 def _row_hashes(a):
+    """tools/make_fullframe_golden.py row_hashes: NaN values hashed as one canonical quiet NaN (their position
+    counts, their payload is not part of the reference's arithmetic)."""
     import hashlib
+    a = np.array(a, copy=True)
+    if a.dtype == np.float32:
+        a = a.view(np.uint32)
+        a[(a & 0x7FFFFFFF) > 0x7F800000] = 0x7FC00000
     return [hashlib.sha256(np.ascontiguousarray(r).tobytes()).hexdigest()[:16] for r in a]
 
 

@@ -24,6 +24,13 @@ OUT = os.path.join(T.GOLDEN, "fullframe_oracle.json")
 
 
 def row_hashes(a):
+    """SHA-256 (16 hex digits) of every row; NaN values hashed as one canonical quiet NaN: the bit pattern of
+    a NaN is not part of the reference's arithmetic (x86 and gfx950 produce different payloads / signs for
+    the same invalid operation), its position is."""
+    a = np.array(a, copy=True)
+    if a.dtype == np.float32:
+        a = a.view(np.uint32)
+        a[(a & 0x7FFFFFFF) > 0x7F800000] = 0x7FC00000
     return [hashlib.sha256(np.ascontiguousarray(r).tobytes()).hexdigest()[:16] for r in a]
 
 
