@@ -111,8 +111,12 @@ __device__ __forceinline__ int xcd_block(uint32_t tune) {
 // start a camera sample, trace a segment, shade, end the path on a miss / Russian roulette /
 // the bounce limit, start its next sample -- so a lane only idles once its whole pixel is
 // done.  The per-pixel draw order (u, v, then 4 draws per hit) is the reference's.
+#ifndef RT_LDS_SL
+#define RT_LDS_SL 16  // stack entries in LDS (4 KB per wave)
+#endif
+
 template <int STACK, bool STATS, int MODE>
-__device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfast::Stack<(STACK < 16 ? STACK : 16)>& stk,
+__device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfast::Stack<(STACK < RT_LDS_SL ? STACK : RT_LDS_SL)>& stk,
                                                  uint32_t* const scratch) {
     if (a.gate && *a.gate != a.gate_value) return;  // foreign scenes: the other tracer renders this frame
     const float4* nodes4 = reinterpret_cast<const float4*>(a.nodes);
@@ -120,9 +124,11 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
     // this lane's pixel: slot k*256 + tid of the launch's list (k < 0: none)
     int x = 0, y = 0;
     bool pixel = false;
-    size_t slot = 0;
-    rt_rng_state* rs = a.rng;
+    // Path state is kept small: it is live across every trace call, where the 7-wave build spills it
+    // (32-bit slot, no RNG pointer: rng_slot() recomputes it; the alpha sum is the sample count)
+    uint32_t slot = 0;  // < 2^32 (rt_render checks slot_count)
     rtm::Xorwow rng{0, 0, 0, 0, 0, 0};
+    auto rng_slot = [&]() { return a.rng + (a.out_shard ? (size_t)slot : (size_t)y * a.width + x); };
     auto bind = [&](int k, int tid) {
         const int tile = k >= 0 ? shard_tile(a, k) : -1;
         int lx, ly;
@@ -130,9 +136,11 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
         x = (tile % a.tiles_x) * TILE + lx;
         y = (tile / a.tiles_x) * TILE + ly;
         pixel = tile >= 0 && x < a.width && y < a.height;
-        slot = (size_t)(k >= 0 ? k : 0) * (TILE * TILE) + tid;
-        rs = a.rng + (a.out_shard ? slot : (size_t)(pixel ? y : 0) * a.width + (pixel ? x : 0));
-        if (pixel) rng = rtm::Xorwow{rs->d, rs->v[0], rs->v[1], rs->v[2], rs->v[3], rs->v[4]};
+        slot = (uint32_t)(k >= 0 ? k : 0) * (TILE * TILE) + (uint32_t)tid;
+        if (pixel) {
+            const rt_rng_state* rs = rng_slot();
+            rng = rtm::Xorwow{rs->d, rs->v[0], rs->v[1], rs->v[2], rs->v[3], rs->v[4]};
+        }
     };
     // entry i of the launch's lane order: the lane map, or slot i (wave i / 64 = 8x8 sub-tile)
     auto bind_entry = [&](long long i) {
@@ -155,7 +163,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
     Counters c;
     const rtm::f3 cam_o = ld3(a.cam.origin), cam_h = ld3(a.cam.horizontal), cam_v = ld3(a.cam.vertical),
                   cam_ll = ld3(a.cam.lower_left_corner);
-    float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f, acc_a = 0.0f;
+    float acc_r = 0.0f, acc_g = 0.0f, acc_b = 0.0f;
     int sample = 0, bounce = 0;
     bool path = false;
     rtm::f3 ro = cam_o, rd = cam_o, color = rtm::mk(0, 0, 0), thr = rtm::mk(1, 1, 1);
@@ -182,7 +190,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
                         base + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                     if ((long long)i < qn) {
                         bind_entry(qbase + (long long)i);
-                        acc_r = acc_g = acc_b = acc_a = 0.0f;
+                        acc_r = acc_g = acc_b = 0.0f;
                         sample = 0;
                     }
                 }
@@ -203,7 +211,6 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
                 bounce = 0;
                 path = true;
                 if (a.bounces == 0) {  // an empty bounce loop: the sample contributes (0,0,0,1)
-                    acc_a += 1.0f;
                     sample++;
                     path = false;
                     continue;
@@ -212,7 +219,9 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
                 pixel = false;
                 // main_raytracing.cu:195-199
                 const float fs = (float)a.spp;
-                const rtm::f4 res{acc_r / fs, acc_g / fs, acc_b / fs, acc_a / fs};
+                // the reference's alpha sum adds 1.0f per sample: (float)sample exactly, and stuck at 2^24
+                // from there on (2^24 + 1 rounds back to 2^24 in fp32)
+                const rtm::f4 res{acc_r / fs, acc_g / fs, acc_b / fs, (float)min(sample, 1 << 24) / fs};
                 const float lerp = a.frame_index > 0 ? 1.0f / (float)(a.frame_index + 1) : 1.0f;
                 float4 prev;
                 float4* out;
@@ -226,6 +235,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
                 }
                 const rtm::f4 o = rtm::mix4(rtm::f4{prev.x, prev.y, prev.z, prev.w}, res, lerp);
                 *out = make_float4(o.x, o.y, o.z, 1.0f);
+                rt_rng_state* rs = rng_slot();
                 rs->d = rng.d;
                 rs->v[0] = rng.v0;
                 rs->v[1] = rng.v1;
@@ -275,7 +285,6 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
             acc_r += color.x;
             acc_g += color.y;
             acc_b += color.z;
-            acc_a += 1.0f;
             sample++;
             path = false;
         }
@@ -362,7 +371,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
 // 0 = _w5, the default; 1 = unconstrained; 2 = _w6; 3 = _w7).
 template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
-    constexpr int SL = STACK < 16 ? STACK : 16;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
+    constexpr int SL = STACK < RT_LDS_SL ? STACK : RT_LDS_SL;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
     __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
     __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
@@ -370,7 +379,7 @@ __global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
 }
 template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(5))) void render_fast_kernel_w5(RenderArgs a) {
-    constexpr int SL = STACK < 16 ? STACK : 16;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
+    constexpr int SL = STACK < RT_LDS_SL ? STACK : RT_LDS_SL;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
     __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
     __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
@@ -378,7 +387,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(5))) void 
 }
 template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(6))) void render_fast_kernel_w6(RenderArgs a) {
-    constexpr int SL = STACK < 16 ? STACK : 16;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
+    constexpr int SL = STACK < RT_LDS_SL ? STACK : RT_LDS_SL;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
     __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
     __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
@@ -386,7 +395,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(6))) void 
 }
 template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(7))) void render_fast_kernel_w7(RenderArgs a) {
-    constexpr int SL = STACK < 16 ? STACK : 16;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
+    constexpr int SL = STACK < RT_LDS_SL ? STACK : RT_LDS_SL;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
     __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
     __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];  // coop_tree's cluster compaction
     uint32_t ovf[STACK > SL ? STACK - SL : 1];

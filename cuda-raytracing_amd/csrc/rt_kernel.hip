@@ -740,6 +740,7 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
         return set_error("rt_render: lane_slots needs a positive multiple of 64 entries (< 2^30)");
     a.lane_slots = p->lane_slots;
     a.slot_count = (long long)tiles * TILE * TILE;
+    if (a.slot_count > (1LL << 32)) return set_error("rt_render: more than 2^32 pixel slots in one launch");
     a.lane_cost = p->lane_cost;
     a.priority_waves = p->lane_slots ? (int)std::min<int64_t>(std::max<int64_t>(p->priority_waves, 0), 1 << 30) : 0;
     const int waves = p->lane_slots ? (int)(p->lane_slot_count / WAVE) : tiles * 4;  // production tracer's grid
