@@ -68,7 +68,7 @@ struct RenderArgs {
     //   4-5 big-leaf mode (launch_fast_t), 7 statistics through the leaf trees, 8 timing frame (phase
     //   clocks), 9-10 occupancy override (1 compiler's choice, 2 = 6, 3 = 7 waves per SIMD),
     //   11 per-wave clock records, 12 no split small steps, 13-15 split threshold, 16-19 XCD run
-    //   length (xcd_block), 20 no twin quads, 21-23 twin rounds' cooperative weight, 26 no lone-ray traversal, 27 the reference's node array instead of the
+    //   length (xcd_block), 20 no twin quads, 21-23 twin rounds' cooperative weight, 24 no deferred leaf trees, 26 no lone-ray traversal, 27 the reference's node array instead of the
     //   mirror's private one (rt_kernel.hip), 28 no big-leaf screens, 30 per-lane leaf-tree walk,
     //   31 subtree order.
     uint32_t tune;

@@ -461,6 +461,27 @@ def test_big_leaf_screens_equal_plain(rt, wps):
     assert np.array_equal(res[0][1], res[1 << 28][1])
 
 
+@pytest.mark.parametrize("wps", [5, 6, 7])
+def test_deferred_tree_leaves_equal_reference_order(rt, wps):
+    """Deferred leaf trees (rt_fast.h defer_leaf: a lane's first tree leaf walked at the end of its
+    traversal, with the bound the rest of the scene left and ties decided by DFS order) render the
+    4-bunny frame and RNG states bit for bit as the walk at the leaf (RT_TUNE bit 24), at every
+    occupancy; the full-frame oracle fixture of config 4 (test_gpu_fullframe.py) covers the default."""
+    w, h, spp, bounces = 256, 144, 4, 6
+    res = {}
+    for tune in (0, 1 << 24):  # bit 24: deferral off
+        s = scene(rt, w, h, "bunny4")
+        rng = rt.alloc_rng(w * h)
+        rt.init_rng_states(rng, w, h, T.SEED)
+        s.upload(rng.data_ptr())
+        a, b = rt.alloc_surface(w, h), rt.alloc_surface(w, h)
+        rt.render(s, a, b, w, h, spp, bounces, 0, waves_per_simd=wps, tune=tune)
+        torch.cuda.synchronize()
+        res[tune] = (rt.surface_view(a, w).cpu().numpy().copy(), rng.cpu().numpy().copy())
+    assert np.array_equal(res[0][0].view(np.uint32), res[1 << 24][0].view(np.uint32))
+    assert np.array_equal(res[0][1], res[1 << 24][1])
+
+
 def test_lone_and_lane_overlap_is_caught(rt):
     """A slot in both lone_slots and lane_slots would be rendered twice at once (undefined results,
     rt_abi.h); RT_RENDER_VALIDATE finds it on the device before anything is launched."""
