@@ -14,6 +14,7 @@ for c in ${CFGS:-cfg1 cfg2 cfg3 cfg4 cfg5}; do
   [ "$c" = "cfg2" ] && extra=""
   timeout -k 10 400 python bench.py --config $c --steps ${STEPS:-5} --warmup 2 --pmc-dir "$R/gpurun_out/pmc_$c" $extra > gpurun_out/bench_${TAG}_$c.log 2>&1
   rc=$?; echo "bench $c exit $rc: $(tail -1 gpurun_out/bench_${TAG}_$c.log | cut -c1-200)"; fatal $rc "bench $c"
+  rm -f "$R/gpurun_out/pmc_$c/lane_map.npy"  # the plan's lane map (33 MB for config 3): not a profile
 done
 if [ -z "${NO_TRACE:-}" ]; then
   cd /tmp
