@@ -157,6 +157,7 @@ SIGNATURES = {
     "rt_scene_mirror_info": (_I, [_P, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
     "rt_scene_mirror_copy": (_I, [_P, _P, _P, _P]),
     "rt_scene_mirror_nodes": (_I, [_P, _P, ctypes.POINTER(_SZ)]),
+    "rt_scene_mirror_face_leaf": (_I, [_P, _P, ctypes.POINTER(_SZ)]),
     "rt_scene_mirror_twins": (_I, [_P, _P, ctypes.POINTER(_SZ), _P, ctypes.POINTER(_SZ)]),
     "rt_mirror_build_check": (_I, [_P, _SZ, _P, _SZ, _P, _SZ, _P, _SZ, _P, ctypes.POINTER(ctypes.c_int)]),
     "rt_cluster_cull_host": (_I, [_P, _P, ctypes.c_float, _P]),
@@ -325,6 +326,17 @@ class Scene:
         _check(lib().rt_scene_mirror_nodes(self.handle, None, ctypes.byref(n)), "rt_scene_mirror_nodes")
         out = np.zeros((n.value, 8), dtype=np.float32)
         _check(lib().rt_scene_mirror_nodes(self.handle, out.ctypes.data, ctypes.byref(n)), "rt_scene_mirror_nodes")
+        return out
+
+    def mirror_face_leaf(self):
+        """Scenes with leaf trees: each face's leaf in the private node array (uint32; 0xffffffff none,
+        0xfffffffe two leaves), the deferred tree leaves' guard table (rt_fast.h); empty otherwise."""
+        import numpy as np
+        n = ctypes.c_size_t()
+        _check(lib().rt_scene_mirror_face_leaf(self.handle, None, ctypes.byref(n)), "rt_scene_mirror_face_leaf")
+        out = np.zeros(n.value, dtype=np.uint32)
+        if n.value:
+            _check(lib().rt_scene_mirror_face_leaf(self.handle, out.ctypes.data, ctypes.byref(n)), "rt_scene_mirror_face_leaf")
         return out
 
     def mirror_twins(self):

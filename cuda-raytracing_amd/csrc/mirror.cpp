@@ -265,6 +265,26 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
     for (uint32_t r : roots) std::memcpy(&out->tree[(size_t)r * 16 + 12], &nl, 4);
     rt_build_treelets(nodes, node_count, out->treelets);
     rt_build_private_nodes(nodes, node_count, out->nodes);
+    // scenes with leaf trees: the leaf (private node) of every face, for the deferred tree leaves' check
+    out->face_leaf.clear();
+    if (!out->tree.empty()) {
+        std::vector<uint32_t> fl(face_count, FACE_NO_LEAF);
+        const size_t nn = out->nodes.size() / 8;
+        for (size_t k = 0; k < nn; k++) {
+            uint32_t first, count;
+            std::memcpy(&first, &out->nodes[k * 8 + 6], 4);
+            std::memcpy(&count, &out->nodes[k * 8 + 7], 4);
+            if (count == 0 || (size_t)first + count > index_count) continue;
+            for (uint32_t i = first; i < first + count; i++) {
+                uint32_t f;
+                std::memcpy(&f, &out->tris[(size_t)i * 12 + 9], 4);
+                if (f >= face_count) continue;
+                fl[f] = fl[f] == FACE_NO_LEAF || fl[f] == (uint32_t)k ? (uint32_t)k : FACE_TWO_LEAVES;
+            }
+        }
+        out->face_leaf.resize(face_count);
+        std::memcpy(out->face_leaf.data(), fl.data(), face_count * 4);
+    }
 }
 
 // The traversal's private node array (mirror.h nodes): the reference's BVH nodes renumbered so
@@ -403,17 +423,17 @@ int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owne
     const std::vector<float> lt = rt_ltris_device_layout(m.ltris);
     // the parts in one block, each starting on a 256-B boundary (pairs of nodes and records on
     // cache-line boundaries: mirror.h)
-    const std::vector<float>* parts[10] = {&m.nodes, &m.tris, &m.pairs, &m.tree, &lt, &m.spairs, &m.flat, &m.treelets, &m.quads,
-                                           &m.units};
-    size_t off[10], total = 0;
-    for (int i = 0; i < 10; i++) {
+    const std::vector<float>* parts[11] = {&m.nodes, &m.tris, &m.pairs, &m.tree, &lt, &m.spairs, &m.flat, &m.treelets, &m.quads,
+                                           &m.units, &m.face_leaf};
+    size_t off[11], total = 0;
+    for (int i = 0; i < 11; i++) {
         off[i] = total;
         total += (parts[i]->size() * 4 + 255) & ~(size_t)255;
     }
     void* block = nullptr;
     if (rt_malloc(&block, total + 256) != 0) return -1;
     char* b = static_cast<char*>(block);
-    for (int i = 0; i < 10; i++)
+    for (int i = 0; i < 11; i++)
         if (!parts[i]->empty() && rt_memcpy_h2d(b + off[i], parts[i]->data(), parts[i]->size() * 4) != 0) {
             rt_free(block);
             return -1;
@@ -430,6 +450,7 @@ int rt_internal_install_mirror(const GPUScene* s, const MirrorHost& m, bool owne
     e.dev.treelets = at(7);
     e.dev.quads = at(8);
     e.dev.units = at(9);
+    e.dev.face_leaf = at(10);
     e.dev.depth = m.depth;
     e.dev.fast = m.fast;
     e.dev.screens = m.screens;

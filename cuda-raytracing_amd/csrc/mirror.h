@@ -61,6 +61,7 @@
 
 constexpr uint32_t MIRROR_BIG_LEAF = 8;     // leaves above this get pair records (== rtfast::BIG)
 constexpr uint32_t MIRROR_TREE_LEAF = 1024;  // ... and leaves this large a leaf tree (leaftree.h) instead
+constexpr uint32_t FACE_NO_LEAF = 0xffffffffu, FACE_TWO_LEAVES = 0xfffffffeu;  // MirrorHost::face_leaf
 
 struct MirrorHost {
     std::vector<float> nodes;     // 8 floats per private node (GPUBVHNode layout)
@@ -73,6 +74,8 @@ struct MirrorHost {
     std::vector<float> ltris;     // 12 floats per leaf-tree triangle record
     std::vector<float> flat;      // 16 floats per record: leaf trees' flat cluster / cut lists
     std::vector<float> treelets;  // 64 slots x 12 floats per treelet (rt_lone.hip)
+    std::vector<float> face_leaf; // scenes with leaf trees: uint32 per face, the private node index of the leaf
+                                  // holding it (FACE_NO_LEAF / FACE_TWO_LEAVES); rt_fast.h deferred tree leaves
     int depth = 0;                // deepest leaf (root = 0) reachable from node 0
     bool fast = true;             // node bounds inside the filtered-slab range (rt_fast.h)
     int screens = 0;              // big leaves with a screen record (pf = 3)
@@ -113,6 +116,7 @@ struct MirrorDevice {
     const void* ltris = nullptr;
     const void* flat = nullptr;
     const void* treelets = nullptr;
+    const void* face_leaf = nullptr;
     int depth = -1;
     bool fast = false;
     int screens = 0;

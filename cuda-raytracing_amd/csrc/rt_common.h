@@ -63,6 +63,7 @@ struct RenderArgs {
     const float4* ltris;  // their triangle records
     const float4* spairs; // small leaves' triangles in packed pairs, pair (i, i+1) at record i, or null
     const float4* flat;   // leaf trees' flat cluster / cut lists (leaftree.h) or null
+    const uint32_t* face_leaf;  // scenes with leaf trees: each face's leaf (mirror.h MirrorHost::face_leaf) or null
     // Diagnostic A/B knobs (rt_render_params.tune; 0 = the production path, every setting exact):
     //   bit 0 no cooperative leaf rounds, 1 no pair records, 2 no leaf trees, 3 no small-leaf pairs,
     //   4-5 big-leaf mode (launch_fast_t), 7 statistics through the leaf trees, 8 timing frame (phase

@@ -1097,18 +1097,26 @@ __device__ __forceinline__ bool small_step(const float4* nodes4, const float4* t
 // Deferred leaf trees (RT_TUNE bit 24 turns them off).  BVHRayHit tests a leaf when it pops it
 // (main_raytracing.cu:51-71), so what a huge leaf hits culls the rest of the traversal.  Here a lane's first
 // tree leaf is skipped and remembered, the traversal goes on, and the leaf is walked at the end with the
-// bound the rest of the scene left -- finite for 80 % of config 4's tree-leaf visits instead of 43 %, and
+// bound the rest of the scene left -- finite for 77 % of config 4's tree-leaf visits instead of 43 %, and
 // 28 % fewer of the leaf's clusters entered below it (tools/defer_probe.c, which checks the rule below
 // against the reference order on every segment of sampled rows: 0 differences).  The result is the
-// reference's: accepts only ever lower `closest`, so the rest visits a superset of the reference's nodes
-// and finds the same best triangle among them; the leaf came first in DFS order, so it wins a tie against
-// a hit found after it (bound just above that hit) and loses one against the hit it was entered with
-// (bound = that hit, unchanged).  A NaN distance after the deferral (where the order of accepts matters)
-// redoes the lane's traversal from the root in the reference order, from the hit the leaf was entered
-// with (nothing before the leaf in DFS order can be accepted again: none is below it).
+// reference's: accepts only ever lower `closest`, so the rest visits a superset of the nodes the reference
+// visits after the leaf; the leaf came first in DFS order, so it wins a tie against a hit found after it
+// (bound just above that hit) and loses one against the hit it was entered with (bound = that hit).  And
+// the reference must still reach the leaf P of the rest's best hit F after walking the leaf first: P's
+// ancestors contain its box, so their rounded slab tmin is at most tmin_P, and it does iff the leaf holds
+// nothing at or below tmin_P -- shown by the walk when tmin_P <= t_F, walked once more when a rounded t_F
+// lies below P's rounded entry (the end phase below; P from the mirror's face -> leaf table).  A NaN
+// distance after the deferral, or a second walk that finds something, redoes the lane's traversal from the
+// root in the reference order, from the hit the leaf was entered with (nothing before the leaf in DFS order
+// can be accepted again: none is below it).
 // LDS per lane, scratch[64 + k * 64 + lane]: k = 0 the leaf's first index (DEFER_NONE: none, DEFER_OFF:
 // deferral off after a redo), 1 its count, 2-6 the hit at the leaf (best bits, kind, id, bx, by).
 constexpr uint32_t DEFER_NONE = 0xffffffffu, DEFER_OFF = 0xfffffffeu;
+
+__device__ __forceinline__ float next_up(float t) {  // the next float above t >= 0 (or -0)
+    return __uint_as_float((__float_as_uint(t) & 0x7fffffffu) + 1u);
+}
 constexpr int DEFER_LDS_WORDS = 64 + 7 * 64;
 
 __device__ __forceinline__ bool defer_leaf(uint32_t* scratch, const Trav& T, const Hit& h) {
@@ -1430,7 +1438,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                                       const float4* tree, const float4* ltris, const float4* flat,
                                       const float4* spairs, uint32_t tune, const S& stk, uint32_t* scratch,
                                       const Ray& R, Hit& h, bool live, C& c, const float4* quads = nullptr,
-                                      const float4* units = nullptr) {
+                                      const float4* units = nullptr, const uint32_t* face_leaf = nullptr) {
     Trav T{0, 0, 0};
     bool active = live && trav_begin<STATS>(nodes4, R, h, T, c);
     // big-leaf screens (screen_leaf, MODE bit 5): split-step variants for scenes that have them
@@ -1540,14 +1548,39 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                     const uint32_t entry = D[128];
                     bool redo = pend && !(h.best == h.best);
                     // a hit found after the leaf loses ties to it: the bound just above that hit
-                    const float bnd = __float_as_uint(h.best) != entry
-                                          ? __uint_as_float((__float_as_uint(h.best) & 0x7fffffffu) + 1u)
-                                          : h.best;
+                    const float bnd = __float_as_uint(h.best) != entry ? next_up(h.best) : h.best;
                     Trav TD;
                     TD.first = pend ? df : 0u, TD.count = pend ? D[64] : 0u, TD.sp = T.sp;
                     const uint32_t root = pend ? __float_as_uint(tris[3 * (size_t)df + 2].z) : 0u;
+                    const uint32_t h1 = __float_as_uint(h.best);
                     const unsigned long long mw = __ballot(pend && !redo);
                     if (mw) coop_tree<TIMING, true>(tris, tree, ltris, flat, mw, root, R, h, TD, scratch, tune, c, bnd, &redo);
+                    // The rest's best hit F came after the leaf and the leaf has nothing at or below it.  The
+                    // reference walked the leaf first, and reaches F's leaf P -- and P's ancestors, whose boxes
+                    // contain P's, so their rounded slab tmin is at most tmin_P -- only if `closest` stayed above
+                    // tmin_P, i.e. if the leaf holds nothing at or below tmin_P.  tmin_P <= t_F: shown by the walk
+                    // above.  tmin_P > t_F (a rounded distance below its own box's rounded entry: a triangle on a
+                    // box face, or an ill-conditioned grazing hit): the leaf once more up to tmin_P, and the
+                    // lane redone in the reference order if that finds anything (or if F's leaf is unknown).
+                    const bool chk = pend && !redo && h1 != entry && __float_as_uint(h.best) == h1 && h.kind == 2;
+                    bool again = false;
+                    float tp = 0.0f;
+                    if (chk) {
+                        const uint32_t P = face_leaf ? face_leaf[h.id] : 0xffffffffu;
+                        if (P >= 0xfffffffeu) {
+                            redo = true;
+                        } else {
+                            float tx;
+                            slab_exact(R, ldo(nodes4, 2 * P), ldo(nodes4, 2 * P + 1), &tp, &tx);
+                            again = tp > h.best;
+                        }
+                    }
+                    const unsigned long long ma = __ballot(again);
+                    if (ma) {
+                        coop_tree<TIMING, true>(tris, tree, ltris, flat, ma, root, R, h, TD, scratch, tune, c, next_up(tp),
+                                                &redo);
+                        if (again && __float_as_uint(h.best) != h1) redo = true;
+                    }
                     if (pend) D[0] = redo ? DEFER_OFF : DEFER_NONE;
                     if (TIMING) {
                         c.cy_tree += __builtin_amdgcn_s_memtime() - td0;

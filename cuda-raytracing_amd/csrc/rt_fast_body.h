@@ -276,7 +276,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
         }
         const rtfast::Ray R = rtfast::make_ray(ro, rd, nd, scene_fast);
         rtfast::trace<STATS, MODE>(nodes4, tris, a.pairs, a.tree, a.ltris, a.flat, a.spairs, a.tune, stk, scratch, R, h,
-                                   path, c, a.quads, a.units);
+                                   path, c, a.quads, a.units, a.face_leaf);
         if (!path) continue;
 
         bool end = shade_segment<STATS>(a, h, ro, rd, nd, rng, color, thr, c);

@@ -466,8 +466,8 @@ void upload_mirror(ForeignBuild* b) {
         rt_build_mirror(nodes, b->bytes[0] / sizeof(GPUBVHNode), fi, b->bytes[1] / 4, faces, b->bytes[2] / sizeof(GPUFace),
                         verts, b->bytes[3] / sizeof(GPUVertex), &mh);
         const std::vector<float> lt = rt_ltris_device_layout(mh.ltris);
-        const std::vector<float>* parts[10] = {&mh.tris, &mh.pairs, &mh.tree, &lt, &mh.spairs, &mh.flat, &mh.treelets, &mh.nodes,
-                                               &mh.quads, &mh.units};
+        const std::vector<float>* parts[11] = {&mh.tris, &mh.pairs, &mh.tree, &lt, &mh.spairs, &mh.flat, &mh.treelets, &mh.nodes,
+                                               &mh.quads, &mh.units, &mh.face_leaf};
         size_t total = 256;  // each part on a 256-B boundary (mirror.h: cache-line aligned pairs)
         for (auto* v : parts) total += (v->size() * 4 + 255) & ~(size_t)255;
         hipStream_t st;
@@ -475,8 +475,8 @@ void upload_mirror(ForeignBuild* b) {
         void* block = nullptr;
         if (hipMallocAsync(&block, total, st) != hipSuccess) throw std::runtime_error("mirror allocation failed");
         char* p = static_cast<char*>(block);
-        const void* where[10];
-        for (int i = 0; i < 10; i++) {
+        const void* where[11];
+        for (int i = 0; i < 11; i++) {
             const size_t nb = parts[i]->size() * 4;
             where[i] = nb ? p : nullptr;
             if (nb && hipMemcpyAsync(p, parts[i]->data(), nb, hipMemcpyHostToDevice, st) != hipSuccess)
@@ -489,7 +489,7 @@ void upload_mirror(ForeignBuild* b) {
         b->block = block;
         b->dev.tris = where[0], b->dev.pairs = where[1], b->dev.tree = where[2], b->dev.ltris = where[3];
         b->dev.spairs = where[4], b->dev.flat = where[5], b->dev.treelets = where[6], b->dev.nodes = where[7];
-        b->dev.quads = where[8], b->dev.units = where[9];
+        b->dev.quads = where[8], b->dev.units = where[9], b->dev.face_leaf = where[10];
         b->dev.depth = mh.depth, b->dev.fast = mh.fast, b->dev.owned = false, b->dev.fingerprint = b->fingerprint;
         b->dev.screens = mh.screens;
         b->state = 2;
@@ -794,6 +794,7 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     a.ltris = (const float4*)mir.ltris;
     a.spairs = (a.tune & 8u) ? nullptr : (const float4*)mir.spairs;
     a.flat = (const float4*)mir.flat;
+    a.face_leaf = (const uint32_t*)mir.face_leaf;
     a.tris = want_ref ? nullptr : (const FlatTri*)tris;
     const bool stats = (p->flags & RT_RENDER_STATS) != 0;
     hipStream_t s = (hipStream_t)stream;

@@ -724,6 +724,13 @@ int rt_scene_mirror_twins(rt_scene* s, float* quads, size_t* quad_count, float* 
     if (units) std::memcpy(units, m.units.data(), m.units.size() * 4);
     return 0;
 }
+int rt_scene_mirror_face_leaf(rt_scene* s, uint32_t* leaf, size_t* count) {
+    MirrorHost m;
+    if (host_mirror(s, &m) != 0) return -1;
+    *count = m.face_leaf.size();
+    if (leaf) std::memcpy(leaf, m.face_leaf.data(), m.face_leaf.size() * 4);
+    return 0;
+}
 void rt_scene_build(rt_scene* s) { s->scene.BuildHost(); }
 void rt_scene_camera(const rt_scene* s, GPUCamera* out) {
     *out = static_cast<const GPUCamera&>(const_cast<Scene&>(s->scene).GetCamera());

@@ -293,3 +293,43 @@ def test_overlapping_big_leaves_get_no_twins():
     for lead in (f, f + 1):
         assert meta2[lead, 1] in (1, 3), f"big leaf at {lead} lost its first-record kind"
     assert meta2[f, 0] != meta2[f + 1, 0], "each big leaf points at its own pairs"
+
+
+def test_face_leaf_table():
+    """The deferred tree leaves' guard table (mirror.h face_leaf, rt_fast.h): for a scene with leaf trees,
+    every face maps to the private node of the one leaf that holds it -- whose box is then the box the
+    reference tests before that face (main_raytracing.cu:43-71) -- checked against the reference arrays
+    walked independently; scenes without leaf trees carry no table."""
+    rt = T.load_rt()
+    s = rt.Scene()
+    s.setup("bunny")
+    s.build()
+    assert s.mirror_face_leaf().size == 0
+    s = rt.Scene()
+    s.setup("bunny4")
+    s.build()
+    fl = s.mirror_face_leaf()
+    arrays = s.host_arrays()
+    ref = arrays["nodes"].view(np.float32).reshape(-1, 8)
+    refu = ref.view(np.uint32)
+    fidx = arrays["face_indices"].view(np.uint32)
+    prv = s.mirror_nodes()
+    prvu = prv.view(np.uint32)
+    assert fl.size == arrays["faces"].size // 16
+    # the reference's leaf of every face, through the same paired DFS as test_private_node_array
+    want = np.full(fl.size, 0xFFFFFFFF, dtype=np.uint64)
+    st = [(0, 0)]
+    while st:
+        a, b = st.pop()
+        if refu[a, 7] > 0:
+            f0, n = int(refu[a, 6]), int(refu[a, 7])
+            faces = fidx[f0:f0 + n]
+            assert np.all(want[faces] == 0xFFFFFFFF), "a face in two leaves"
+            want[faces] = b
+            assert np.array_equal(ref[a, :6].view(np.uint32), prv[b, :6].view(np.uint32))
+            continue
+        fa, fb = int(refu[a, 6]), int(prvu[b, 6])
+        st.append((fa, fb))
+        st.append((fa + 1, fb + 1))
+    assert np.array_equal(fl.astype(np.uint64), want)
+    assert np.count_nonzero(fl == 0xFFFFFFFF) == 0

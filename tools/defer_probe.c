@@ -7,8 +7,10 @@
  * superset of the reference's nodes); at the end the leaf is tested against the bound the rest of the
  * scene left.  The result is the reference's if the leaf wins ties against a hit found after the leaf
  * in DFS order (the reference would have tested the leaf first, and an equal distance later is not
- * accepted) and loses them against one found before it; a NaN distance anywhere after the leaf falls
- * back to the reference order.  This tool checks that rule against the oracle's own traversal on
+ * accepted) and loses them against one found before it, PROVIDED the reference still reaches the leaf of
+ * that later hit: when the hit's rounded distance lies below its own leaf box's rounded entry tmin, the
+ * leaf must hold nothing at or below that tmin (the guard, as rt_fast.h: a second walk; otherwise the
+ * reference order); a NaN distance anywhere after the leaf falls back to the reference order too.  This tool checks that rule against the oracle's own traversal on
  * every segment of sampled rows and prices it: node visits, and the giant leaf's triangles whose own
  * bounding box the ray enters below the bound (a proxy for the leaf tree's cull) at the leaf's entry
  * distance vs at the end-of-traversal bound.
@@ -76,6 +78,18 @@ static void build_clusters(const OScene* s) {
 }
 
 typedef struct { float t; int kind; uint32_t id; } Res;  /* kind 0 none, 1 sphere, 2 triangle */
+
+/* IntersectAABB's rounded entry parameter (Math.h:50-61 arithmetic, as aabb_hit) */
+static float aabb_tmin(v3 o, v3 d, const ONode* n) {
+    float tx1 = (n->bmin[0] - o.x) / d.x, tx2 = (n->bmax[0] - o.x) / d.x;
+    float tmin = fminf(tx1, tx2);
+    float ty1 = (n->bmin[1] - o.y) / d.y, ty2 = (n->bmax[1] - o.y) / d.y;
+    tmin = fmaxf(tmin, fminf(ty1, ty2));
+    float tz1 = (n->bmin[2] - o.z) / d.z, tz2 = (n->bmax[2] - o.z) / d.z;
+    tmin = fmaxf(tmin, fminf(tz1, tz2));
+    return tmin;
+}
+static uint64_t g_again, g_redo;  /* the guard (rt_fast.h): second walks, and lanes redone in reference order */
 
 static int tri_box_hit(const OScene* s, uint32_t fi, v3 ro, v3 rd, float bound) {
     const OFace* f = &s->faces[fi];
@@ -146,7 +160,7 @@ static Res def_hit(const OScene* s, v3 ro, v3 rd, uint64_t* nodes, uint64_t* tri
     const v3 nd = vnorm(rd);
     Res r;
     spheres(s, ro, nd, &r);
-    uint32_t giant = UINT32_MAX;
+    uint32_t giant = UINT32_MAX, leaf_f = UINT32_MAX;
     int changed = 0, nan_after = 0;
     uint32_t stack[64];
     int top = 0;
@@ -168,7 +182,7 @@ static Res def_hit(const OScene* s, v3 ro, v3 rd, uint64_t* nodes, uint64_t* tri
                 if (tri_t(s, s->face_idx[n->first + i], ro, nd, &t)) {
                     if (t >= r.t || t < 0.0f) continue;
                     r.t = t, r.kind = 2, r.id = s->face_idx[n->first + i];
-                    if (giant != UINT32_MAX) changed = 1, nan_after |= (t != t);
+                    if (giant != UINT32_MAX) changed = 1, nan_after |= (t != t), leaf_f = ni;
                 }
             }
         } else {
@@ -196,6 +210,24 @@ static Res def_hit(const OScene* s, v3 ro, v3 rd, uint64_t* nodes, uint64_t* tri
         }
     }
     if (nan_after) *nan_fb = 1;
+    /* the guard: the leaf found nothing and the rest's best came after it -- the reference reaches that
+       best's leaf only if the deferred leaf holds nothing at or below the leaf's rounded entry tmin */
+    if (changed && !*leaf_won && leaf_f != UINT32_MAX) {
+        const float tp = aabb_tmin(ro, rd, &s->nodes[leaf_f]);
+        if (tp > r.t) {
+#pragma omp atomic
+            g_again++;
+            for (uint32_t i = 0; i < n->count; i++) {
+                float t;
+                if (tri_t(s, s->face_idx[n->first + i], ro, nd, &t) && !(t > tp || t < 0.0f)) {
+                    *nan_fb = 1;  /* redone in the reference order */
+#pragma omp atomic
+                    g_redo++;
+                    break;
+                }
+            }
+        }
+    }
     return r;
 }
 
@@ -315,13 +347,14 @@ int main(int argc, char** argv) {
     printf("{\"scene\": %d, \"width\": %d, \"height\": %d, \"spp\": %d, \"row_step\": %d, \"segments\": %llu, "
            "\"giant_segments\": %llu, \"mismatches\": %llu, \"nan_fallbacks\": %llu, \"leaf_won\": %llu, "
            "\"entry_bound_finite\": %llu, \"end_bound_finite\": %llu, \"nodes_ref\": %llu, \"nodes_deferred\": %llu, "
-           "\"tris_ref\": %llu, \"tris_deferred\": %llu, \"leaf_boxes_at_entry\": %llu, \"leaf_boxes_at_end\": %llu, \"giant_leaves\": %d, \"clusters_at_entry\": %llu, \"clusters_at_end\": %llu, \"leaf_box_culled_at_end\": %llu}\n",
+           "\"tris_ref\": %llu, \"tris_deferred\": %llu, \"leaf_boxes_at_entry\": %llu, \"leaf_boxes_at_end\": %llu, \"giant_leaves\": %d, \"clusters_at_entry\": %llu, \"clusters_at_end\": %llu, \"leaf_box_culled_at_end\": %llu, \"guard_second_walks\": %llu, \"guard_redone\": %llu}\n",
            which, w, hgt, spp, step, (unsigned long long)tot.segs, (unsigned long long)tot.giant_segs,
            (unsigned long long)tot.mism, (unsigned long long)tot.nan_fallback, (unsigned long long)tot.leaf_won,
            (unsigned long long)tot.entry_finite, (unsigned long long)tot.end_finite, (unsigned long long)tot.nodes_ref,
            (unsigned long long)tot.nodes_def, (unsigned long long)tot.tris_ref, (unsigned long long)tot.tris_def,
            (unsigned long long)tot.boxes_entry, (unsigned long long)tot.boxes_end, g_ncl, (unsigned long long)tot.cl_entry,
-           (unsigned long long)tot.cl_end, (unsigned long long)tot.leaf_culled_end);
+           (unsigned long long)tot.cl_end, (unsigned long long)tot.leaf_culled_end, (unsigned long long)g_again,
+           (unsigned long long)g_redo);
     if (g_rays) fclose(g_rays);
     oracle_scene_destroy(s);
     return 0;
