@@ -1060,40 +1060,6 @@ __device__ __forceinline__ bool screen_leaf(const float4* tris, const float4* pa
     return true;
 }
 
-// One small step of a lane at a small leaf or an inner node; false when the traversal is over.
-// (Testing a small leaf in the same step as the inner node that entered it was measured slower:
-// 22.2 vs 20.6 ms, the extra divergence costs more than the saved iterations.)
-template <bool STATS, bool SCR = false, class S, class C>
-__device__ __forceinline__ bool small_step(const float4* nodes4, const float4* tris, const float4* spairs, const S& stk,
-                                           const Ray& R, Hit& h, Trav& T, C& c, const float4* pairs = nullptr) {
-    if constexpr (SCR) {
-        if (T.count > (uint32_t)BIG) {  // a big leaf just reached: its screen, else wait for the round
-            if (!screen_leaf<STATS>(tris, pairs, R, h, T, c)) {
-                T.sp |= SCREENED;
-                return true;
-            }
-            return pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
-        }
-    }
-    if (T.count > 0) {
-        if (!STATS && spairs) {
-            // two triangles per packed pair record (mirror.h spairs), in leaf order
-            for (uint32_t i = T.first; i < T.first + T.count; i += 2) pair_test(R, ld_pair(spairs, i), h);
-        } else {
-            for (uint32_t i = T.first; i < T.first + T.count; i++)
-                test_triangle<STATS>(R, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], h, c);
-        }
-        return pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
-    }
-    if (inner_step<STATS>(nodes4, stk, T.sp, R, h.best, T.first, T.count, c)) return true;
-    return pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
-}
-
-// One big-leaf round, called by all lanes of the wave in converged control flow.  `big` = the
-// lanes waiting at a big leaf (`waiting` on this lane).  The lanes at the leaf of the lowest
-// waiting lane run it together (pairs / cooperative rounds / scalar loads); if every waiting
-// lane is at that leaf, or each lane alone otherwise (MODE: see trace).  Returns whether this
-// lane ran its leaf (it then pops; the others keep waiting).
 // Deferred leaf trees (RT_TUNE bit 24 turns them off).  BVHRayHit tests a leaf when it pops it
 // (main_raytracing.cu:51-71), so what a huge leaf hits culls the rest of the traversal.  Here a lane's first
 // tree leaf is skipped and remembered, the traversal goes on, and the leaf is walked at the end with the
@@ -1127,6 +1093,62 @@ __device__ __forceinline__ bool defer_leaf(uint32_t* scratch, const Trav& T, con
     return true;
 }
 
+// defer_leaf for a lane that has just reached a big leaf, if it is a tree leaf (lead record pf == 2)
+__device__ __forceinline__ bool defer_tree_leaf(const float4* tris, uint32_t* scratch, const Trav& T, const Hit& h) {
+    if (!scratch) return false;
+    if (__float_as_uint(tris[3 * (size_t)T.first + 2].w) != 2u) return false;
+    return defer_leaf(scratch, T, h);
+}
+
+// pop, then: a tree leaf popped as the lane's first is deferred (defer_leaf) and popping goes on
+template <bool DEFER, class S>
+__device__ __forceinline__ bool pop_d(const float4* nodes4, const float4* tris, uint32_t* scratch, const S& stk, const Ray& R,
+                                      const Hit& h, Trav& T) {
+    for (;;) {
+        if (!pop(nodes4, stk, T.sp, R, h.best, T.first, T.count)) return false;
+        if (!DEFER || T.count <= (uint32_t)BIG || !defer_tree_leaf(tris, scratch, T, h)) return true;
+    }
+}
+
+// One small step of a lane at a small leaf or an inner node; false when the traversal is over.
+// (Testing a small leaf in the same step as the inner node that entered it was measured slower:
+// 22.2 vs 20.6 ms, the extra divergence costs more than the saved iterations.)
+// DEF (leaf-tree kernels, RT_TUNE bit 24 clear): a tree leaf the lane reaches as its first is deferred at once
+// (defer_leaf), so the lane steps on instead of waiting for the wave's big-leaf round.
+template <bool STATS, bool SCR = false, bool DEF = false, class S, class C>
+__device__ __forceinline__ bool small_step(const float4* nodes4, const float4* tris, const float4* spairs, const S& stk,
+                                           const Ray& R, Hit& h, Trav& T, C& c, const float4* pairs = nullptr,
+                                           uint32_t* scratch = nullptr) {
+    if constexpr (SCR) {
+        if (T.count > (uint32_t)BIG) {  // a big leaf just reached: its screen, else wait for the round
+            if (!screen_leaf<STATS>(tris, pairs, R, h, T, c)) {
+                T.sp |= SCREENED;
+                return true;
+            }
+            return pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
+        }
+    }
+    if (T.count > 0) {
+        if (!STATS && spairs) {
+            // two triangles per packed pair record (mirror.h spairs), in leaf order
+            for (uint32_t i = T.first; i < T.first + T.count; i += 2) pair_test(R, ld_pair(spairs, i), h);
+        } else {
+            for (uint32_t i = T.first; i < T.first + T.count; i++)
+                test_triangle<STATS>(R, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], h, c);
+        }
+        if constexpr (!DEF) return pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
+    } else if (inner_step<STATS>(nodes4, stk, T.sp, R, h.best, T.first, T.count, c)) {
+        if (!DEF || T.count <= (uint32_t)BIG || !defer_tree_leaf(tris, scratch, T, h)) return true;
+    }
+    if constexpr (!DEF) return pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
+    else return pop_d<DEF>(nodes4, tris, scratch, stk, R, h, T);
+}
+
+// One big-leaf round, called by all lanes of the wave in converged control flow.  `big` = the
+// lanes waiting at a big leaf (`waiting` on this lane).  The lanes at the leaf of the lowest
+// waiting lane run it together (pairs / cooperative rounds / scalar loads); if every waiting
+// lane is at that leaf, or each lane alone otherwise (MODE: see trace).  Returns whether this
+// lane ran its leaf (it then pops; the others keep waiting).
 template <bool STATS, int MODE, bool DEFER = false, class C>
 __device__ __forceinline__ bool big_round(const float4* tris, const float4* pairs, const float4* quads, const float4* units,
                                           const float4* tree,
@@ -1446,6 +1468,8 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
     constexpr bool TIMING = (MODE & 8) != 0;
     constexpr bool DEFER = !STATS && (MODE & 4) != 0;  // leaf-tree scenes: deferred tree leaves
     if constexpr (DEFER) scratch[64 + (threadIdx.x & 63u)] = DEFER_NONE;
+    // deferral at arrival (small_step, pop_d): the scratch to defer into, or null when it is off
+    uint32_t* const dscr = (DEFER && flat && (tune & 0x41000000u) == 0) ? scratch : nullptr;
     unsigned long long t0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
     for (;;) {
         if constexpr ((MODE & 16) != 0) {
@@ -1489,7 +1513,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                 // exists to gather lanes per kind, which matters little when both groups are small)
                 if (!scr_on && mI && mL && nI + nL <= (uint32_t)RT_COMBINE_T) {
                     if (inner || leafs) {
-                        active = small_step<STATS>(nodes4, tris, spairs, stk, R, h, T, c);
+                        active = small_step<STATS, false, DEFER>(nodes4, tris, spairs, stk, R, h, T, c, nullptr, dscr);
                         if (TIMING) c.lane_work++;
                     }
                 } else
@@ -1500,7 +1524,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                         if (TIMING) c.lane_work++;
                     }
                 } else if (inner) {
-                    active = small_step<STATS>(nodes4, tris, spairs, stk, R, h, T, c);
+                    active = small_step<STATS, false, DEFER>(nodes4, tris, spairs, stk, R, h, T, c, nullptr, dscr);
                     if (TIMING) c.lane_work++;
                 }
 #ifdef RT_LANE_HIST
@@ -1604,7 +1628,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
             // a big leaf run alone (cooperative round) costs about as much as 3 small steps
             if (TIMING) c.lane_work += 3;
             if constexpr (scr_on) T.sp &= ~SCREENED;
-            active = pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
+            active = pop_d<DEFER>(nodes4, tris, dscr, stk, R, h, T);
         }
         if (TIMING) {
             const unsigned long long t1 = __builtin_amdgcn_s_memtime();
