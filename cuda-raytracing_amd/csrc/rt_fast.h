@@ -1072,10 +1072,11 @@ __device__ __forceinline__ bool screen_leaf(const float4* tris, const float4* pa
 // the reference must still reach the leaf P of the rest's best hit F after walking the leaf first: P's
 // ancestors contain its box, so their rounded slab tmin is at most tmin_P, and it does iff the leaf holds
 // nothing at or below tmin_P -- shown by the walk when tmin_P <= t_F, walked once more when a rounded t_F
-// lies below P's rounded entry (the end phase below; P from the mirror's face -> leaf table).  A NaN
-// distance after the deferral, or a second walk that finds something, redoes the lane's traversal from the
-// root in the reference order, from the hit the leaf was entered with (nothing before the leaf in DFS order
-// can be accepted again: none is below it).
+// lies below P's rounded entry (the end phase below; P from the mirror's face -> leaf table).  A second
+// walk that finds something redoes the lane's traversal from the root in the reference order, from the hit
+// the leaf was entered with (nothing before the leaf in DFS order can be accepted again: none is below it).
+// NaN distances, whose place in the order of accepts would matter, cannot arise for a deferred ray
+// (defer_leaf's +-2^16 bound); a NaN `closest` at the end redoes the lane all the same.
 // LDS per lane, scratch[64 + k * 64 + lane]: k = 0 the leaf's first index (DEFER_NONE: none, DEFER_OFF:
 // deferral off after a redo), 1 its count, 2-6 the hit at the leaf (best bits, kind, id, bx, by).
 constexpr uint32_t DEFER_NONE = 0xffffffffu, DEFER_OFF = 0xfffffffeu;
@@ -1085,19 +1086,29 @@ __device__ __forceinline__ float next_up(float t) {  // the next float above t >
 }
 constexpr int DEFER_LDS_WORDS = 64 + 7 * 64;
 
-__device__ __forceinline__ bool defer_leaf(uint32_t* scratch, const Trav& T, const Hit& h) {
+// Only rays and scenes inside +-2^16 defer (the ray's origin; the scene's root box, scalar loads): every
+// product of the slab and triangle tests is then finite, so no NaN distance -- whose place in the order of
+// accepts would matter -- can arise after the deferral.
+__device__ __forceinline__ bool defer_leaf(uint32_t* scratch, const float4* nodes4, const Trav& T, const Ray& R,
+                                           const Hit& h) {
     uint32_t* D = scratch + 64 + (threadIdx.x & 63u);
-    if (D[0] != DEFER_NONE || !(h.best == h.best)) return false;
+    if (D[0] != DEFER_NONE || !(h.best <= 1e30f) || !R.fast) return false;
+    const f4v lo = ((ConstF4)nodes4)[0], hi = ((ConstF4)nodes4)[1];
+    const float sc = fmaxf(fmaxf(fmaxf(fabsf(lo.x), fabsf(lo.y)), fmaxf(fabsf(lo.z), fabsf(lo.w))),
+                           fmaxf(fabsf(hi.x), fabsf(hi.y)));
+    const float ro = fmaxf(fmaxf(fabsf(R.o.x), fabsf(R.o.y)), fabsf(R.o.z));
+    if (!(sc < 0x1p16f && ro < 0x1p16f)) return false;
     D[0] = T.first, D[64] = T.count, D[128] = __float_as_uint(h.best), D[192] = (uint32_t)h.kind, D[256] = h.id;
     D[320] = __float_as_uint(h.bx), D[384] = __float_as_uint(h.by);
     return true;
 }
 
 // defer_leaf for a lane that has just reached a big leaf, if it is a tree leaf (lead record pf == 2)
-__device__ __forceinline__ bool defer_tree_leaf(const float4* tris, uint32_t* scratch, const Trav& T, const Hit& h) {
+__device__ __forceinline__ bool defer_tree_leaf(const float4* tris, const float4* nodes4, uint32_t* scratch, const Trav& T,
+                                                const Ray& R, const Hit& h) {
     if (!scratch) return false;
     if (__float_as_uint(tris[3 * (size_t)T.first + 2].w) != 2u) return false;
-    return defer_leaf(scratch, T, h);
+    return defer_leaf(scratch, nodes4, T, R, h);
 }
 
 // pop, then: a tree leaf popped as the lane's first is deferred (defer_leaf) and popping goes on
@@ -1106,7 +1117,7 @@ __device__ __forceinline__ bool pop_d(const float4* nodes4, const float4* tris, 
                                       const Hit& h, Trav& T) {
     for (;;) {
         if (!pop(nodes4, stk, T.sp, R, h.best, T.first, T.count)) return false;
-        if (!DEFER || T.count <= (uint32_t)BIG || !defer_tree_leaf(tris, scratch, T, h)) return true;
+        if (!DEFER || T.count <= (uint32_t)BIG || !defer_tree_leaf(tris, nodes4, scratch, T, R, h)) return true;
     }
 }
 
@@ -1138,7 +1149,7 @@ __device__ __forceinline__ bool small_step(const float4* nodes4, const float4* t
         }
         if constexpr (!DEF) return pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
     } else if (inner_step<STATS>(nodes4, stk, T.sp, R, h.best, T.first, T.count, c)) {
-        if (!DEF || T.count <= (uint32_t)BIG || !defer_tree_leaf(tris, scratch, T, h)) return true;
+        if (!DEF || T.count <= (uint32_t)BIG || !defer_tree_leaf(tris, nodes4, scratch, T, R, h)) return true;
     }
     if constexpr (!DEF) return pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
     else return pop_d<DEF>(nodes4, tris, scratch, stk, R, h, T);
@@ -1154,7 +1165,7 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
                                           const float4* tree,
                                           const float4* ltris, const float4* flat, uint32_t* scratch, uint32_t tune,
                                           unsigned long long big, bool waiting,
-                                          const Ray& R, Hit& h, const Trav& T, C& c) {
+                                          const Ray& R, Hit& h, const Trav& T, C& c, const float4* nodes4 = nullptr) {
     if ((MODE & 4) && tree) {  // MODE bit 2: the scene has leaf trees
         // lanes at leaves with a leaf tree (mirror.h: lead record pf == 2) walk it on their own
         bool at_tree = false;
@@ -1169,7 +1180,7 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
             if constexpr (DEFER) {
                 // a lane's first tree leaf is deferred to the end of its traversal (defer_leaf)
                 if (flat && (tune & 0x41000000u) == 0) {
-                    const bool dfr = at_tree && defer_leaf(scratch, T, h);
+                    const bool dfr = at_tree && defer_leaf(scratch, nodes4, T, R, h);
                     mt = __ballot(at_tree && !dfr);
                     if (!mt) return at_tree;
                 }
@@ -1624,7 +1635,8 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
             }
             break;
         }
-        if (big_round<STATS, MODE, DEFER>(tris, pairs, quads, units, tree, ltris, flat, scratch, tune, big, active, R, h, T, c)) {
+        if (big_round<STATS, MODE, DEFER>(tris, pairs, quads, units, tree, ltris, flat, scratch, tune, big, active, R, h, T, c,
+                                          nodes4)) {
             // a big leaf run alone (cooperative round) costs about as much as 3 small steps
             if (TIMING) c.lane_work += 3;
             if constexpr (scr_on) T.sp &= ~SCREENED;
