@@ -1480,7 +1480,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
     constexpr bool DEFER = !STATS && (MODE & 4) != 0;  // leaf-tree scenes: deferred tree leaves
     if constexpr (DEFER) scratch[64 + (threadIdx.x & 63u)] = DEFER_NONE;
     // deferral at arrival (small_step, pop_d): the scratch to defer into, or null when it is off
-    uint32_t* const dscr = (DEFER && flat && (tune & 0x41000000u) == 0) ? scratch : nullptr;
+    uint32_t* const dscr = (DEFER && tree && flat && (tune & 0x41000000u) == 0) ? scratch : nullptr;
     unsigned long long t0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
     for (;;) {
         if constexpr ((MODE & 16) != 0) {

@@ -117,7 +117,7 @@ int main(int argc, char** argv) {
             return make_float4(q[0], q[1], q[2], q[3]);
         };
         uint64_t reason[7] = {0, 0, 0, 0, 0, 0, 0};
-        uint64_t screen = 0, crounds = 0, trounds = 0, ctests = 0, surv_sub = 0, surv_cl = 0, mism = 0, tris_tested = 0;
+        uint64_t all_cl = 0, all_rounds = 0, prounds = 0, screen = 0, crounds = 0, trounds = 0, ctests = 0, surv_sub = 0, surv_cl = 0, mism = 0, tris_tested = 0;
         for (uint32_t ri = 0; ri < nr; ri++) {
             const float* q = &rays[(size_t)ri * 9];
             rtfast::Ray R;
@@ -157,6 +157,9 @@ int main(int argc, char** argv) {
                     }
                     surv_cl += cls.size();
                     trounds += (cls.size() + (64 / kClusterMax) - 1) / (64 / kClusterMax);
+                    uint32_t ntri = 0;
+                    for (uint32_t ci : cls) ntri += U(fld(cb, nc, ci, 3).w) >> 8;
+                    prounds += (ntri + 63) / 64;  // the same triangles packed 64 to a round
                     for (uint32_t ci : cls) {
                         const float4 Q3 = fld(cb, nc, ci, 3);
                         const uint32_t tb = U(Q3.z), cnt = U(Q3.w) >> 8;
@@ -164,6 +167,22 @@ int main(int argc, char** argv) {
                     }
                     if (L.found) cbest = fminf(cbest, F(U(L.t) + 1u));
                 }
+            }
+            {  // variant: every surviving cluster of the ray first (bound not tightened), then its triangles packed
+                uint32_t ntri = 0, ncl = 0;
+                for (uint32_t k = 0; k < nk; k++) {
+                    const float4 K3 = fld(kb, nk, k, 3);
+                    if ((U(K3.w) & 1u) && rtfast::cluster_cull(R, R.r, b0, fld(kb, nk, k, 0), fld(kb, nk, k, 1), fld(kb, nk, k, 2), K3))
+                        continue;
+                    for (uint32_t ci = U(K3.y); ci < U(K3.z); ci++) {
+                        const float4 Q3 = fld(cb, nc, ci, 3);
+                        if ((U(Q3.w) & 1u) &&
+                            rtfast::cluster_cull(R, R.r, b0, fld(cb, nc, ci, 0), fld(cb, nc, ci, 1), fld(cb, nc, ci, 2), Q3))
+                            continue;
+                        ncl++, ntri += U(Q3.w) >> 8;
+                    }
+                }
+                all_cl += ncl, all_rounds += (ntri + 63) / 64;
             }
             // the sequential loop over the leaf from the same bound (rt_fast.h leaf order = record j)
             if (ri % 16 == 0) {
@@ -176,11 +195,11 @@ int main(int argc, char** argv) {
                "\"cuts\": %u, \"rays\": %u, \"screen_rounds\": %.3f, \"cluster_rounds\": %.3f, \"tri_rounds\": %.3f, "
                "\"cluster_tests\": %.2f, \"surviving_subtrees\": %.2f, \"surviving_clusters\": %.2f, \"tris_tested\": %.1f, "
                "\"checked_mismatches\": %llu, \"kept_cone\": %.2f, \"kept_grown_box\": %.2f, \"kept_box\": %.2f, "
-               "\"kept_uncullable\": %.2f, \"kept_cone_sliver\": %.2f, \"kept_cone_other\": %.2f}\n",
+               "\"kept_uncullable\": %.2f, \"kept_cone_sliver\": %.2f, \"kept_cone_other\": %.2f, \"packed_tri_rounds\": %.3f, \"untightened_clusters\": %.2f, \"untightened_packed_rounds\": %.3f}\n",
                prm.cluster_max, prm.split_angle, prm.min_cull_cos, prm.cut_clusters, nc, nk, nr, (double)screen / nr,
                (double)crounds / nr, (double)trounds / nr, (double)ctests / nr, (double)surv_sub / nr, (double)surv_cl / nr,
                (double)tris_tested / nr, (unsigned long long)mism, (double)reason[1] / nr, (double)reason[2] / nr,
-               (double)reason[3] / nr, (double)reason[4] / nr, (double)reason[5] / nr, (double)reason[6] / nr);
+               (double)reason[3] / nr, (double)reason[4] / nr, (double)reason[5] / nr, (double)reason[6] / nr, (double)prounds / nr, (double)all_cl / nr, (double)all_rounds / nr);
         fflush(stdout);
     }
     return 0;
