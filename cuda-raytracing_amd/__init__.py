@@ -329,8 +329,8 @@ class Scene:
         return out
 
     def mirror_face_leaf(self):
-        """Scenes with leaf trees: each face's leaf in the private node array (uint32; 0xffffffff none,
-        0xfffffffe two leaves), the deferred tree leaves' guard table (rt_fast.h); empty otherwise."""
+        """Scenes with big leaves: each face's leaf in the private node array (uint32; 0xffffffff none,
+        0xfffffffe two leaves), the deferred leaves' guard table (rt_fast.h); empty otherwise."""
         import numpy as np
         n = ctypes.c_size_t()
         _check(lib().rt_scene_mirror_face_leaf(self.handle, None, ctypes.byref(n)), "rt_scene_mirror_face_leaf")

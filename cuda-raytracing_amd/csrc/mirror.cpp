@@ -265,9 +265,9 @@ void rt_build_mirror(const GPUBVHNode* nodes, size_t node_count, const uint32_t*
     for (uint32_t r : roots) std::memcpy(&out->tree[(size_t)r * 16 + 12], &nl, 4);
     rt_build_treelets(nodes, node_count, out->treelets);
     rt_build_private_nodes(nodes, node_count, out->nodes);
-    // scenes with leaf trees: the leaf (private node) of every face, for the deferred tree leaves' check
+    // scenes with big leaves: the leaf (private node) of every face, for the deferred leaves' guard (rt_fast.h)
     out->face_leaf.clear();
-    if (!out->tree.empty()) {
+    if (!out->pairs.empty() || !out->tree.empty()) {
         std::vector<uint32_t> fl(face_count, FACE_NO_LEAF);
         const size_t nn = out->nodes.size() / 8;
         for (size_t k = 0; k < nn; k++) {

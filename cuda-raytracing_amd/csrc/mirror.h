@@ -74,8 +74,8 @@ struct MirrorHost {
     std::vector<float> ltris;     // 12 floats per leaf-tree triangle record
     std::vector<float> flat;      // 16 floats per record: leaf trees' flat cluster / cut lists
     std::vector<float> treelets;  // 64 slots x 12 floats per treelet (rt_lone.hip)
-    std::vector<float> face_leaf; // scenes with leaf trees: uint32 per face, the private node index of the leaf
-                                  // holding it (FACE_NO_LEAF / FACE_TWO_LEAVES); rt_fast.h deferred tree leaves
+    std::vector<float> face_leaf; // scenes with big leaves: uint32 per face, the private node index of the leaf
+                                  // holding it (FACE_NO_LEAF / FACE_TWO_LEAVES); rt_fast.h deferred leaves' guard
     int depth = 0;                // deepest leaf (root = 0) reachable from node 0
     bool fast = true;             // node bounds inside the filtered-slab range (rt_fast.h)
     int screens = 0;              // big leaves with a screen record (pf = 3)

@@ -864,13 +864,11 @@ __device__ __forceinline__ f3 bcast3(f3 v, int lane) {
     return rtm::mk(bcast(v.x, lane), bcast(v.y, lane), bcast(v.z, lane));
 }
 
-// bnd_l: the lane's starting bound (h.best, or just above it for a deferred leaf, below).  END: a deferred
-// leaf's walk at the end of the traversal, where a NaN distance asks for the lane's traversal to be redone
-// in the reference order (*redo) instead of the sequential loop over the leaf.
-template <bool TIMING, bool END = false, class C>
+// bnd_l: the lane's starting bound (its `closest`).
+template <bool TIMING, class C>
 __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree, const float4* ltris, const float4* flat,
                                           unsigned long long m, uint32_t root_l, const Ray& R, Hit& h, const Trav& T,
-                                          uint32_t* scratch, uint32_t tune, C& c, float bnd_l, bool* redo = nullptr) {
+                                          uint32_t* scratch, uint32_t tune, C& c, float bnd_l) {
     const uint32_t lane = threadIdx.x & 63u;
     // RT_TUNE bit 31: visit surviving subtrees nearest box first (costs more than it saves here:
     // 117 vs 111 ms on the 4-bunny frame), else in tree order
@@ -991,10 +989,6 @@ __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree
             }
         }
         if (__ballot(L.nan)) {
-            if constexpr (END) {  // a deferred leaf: the lane's traversal is redone in the reference order
-                if ((int)lane == r) *redo = true;
-                continue;
-            }
             // sequential fallback for this ray (never taken for finite scenes)
             if ((int)lane == r) {
                 for (uint32_t q = f0; q < f0 + c0; q++) {
@@ -1060,76 +1054,62 @@ __device__ __forceinline__ bool screen_leaf(const float4* tris, const float4* pa
     return true;
 }
 
-// Deferred leaf trees (RT_TUNE bit 24 turns them off).  BVHRayHit tests a leaf when it pops it
-// (main_raytracing.cu:51-71), so what a huge leaf hits culls the rest of the traversal.  Here a lane's first
-// tree leaf is skipped and remembered, the traversal goes on, and the leaf is walked at the end with the
-// bound the rest of the scene left -- finite for 77 % of config 4's tree-leaf visits instead of 43 %, and
-// 28 % fewer of the leaf's clusters entered below it (tools/defer_probe.c, which checks the rule below
-// against the reference order on every segment of sampled rows: 0 differences).  The result is the
-// reference's: accepts only ever lower `closest`, so the rest visits a superset of the nodes the reference
-// visits after the leaf; the leaf came first in DFS order, so it wins a tie against a hit found after it
-// (bound just above that hit) and loses one against the hit it was entered with (bound = that hit).  And
-// the reference must still reach the leaf P of the rest's best hit F after walking the leaf first: P's
-// ancestors contain its box, so their rounded slab tmin is at most tmin_P, and it does iff the leaf holds
-// nothing at or below tmin_P -- shown by the walk when tmin_P <= t_F, walked once more when a rounded t_F
-// lies below P's rounded entry (the end phase below; P from the mirror's face -> leaf table).  A second
-// walk that finds something redoes the lane's traversal from the root in the reference order, from the hit
-// the leaf was entered with (nothing before the leaf in DFS order can be accepted again: none is below it).
-// NaN distances, whose place in the order of accepts would matter, cannot arise for a deferred ray
-// (defer_leaf's +-2^16 bound); a NaN `closest` at the end redoes the lane all the same.
-// LDS per lane, scratch[64 + k * 64 + lane]: k = 0 the leaf's first index (DEFER_NONE: none, DEFER_OFF:
-// deferral off after a redo), 1 its count, 2-6 the hit at the leaf (best bits, kind, id, bx, by).
-constexpr uint32_t DEFER_NONE = 0xffffffffu, DEFER_OFF = 0xfffffffeu;
+// Deferred big leaves (RT_TUNE bit 24 turns them off).  BVHRayHit tests a leaf when it pops it
+// (main_raytracing.cu:51-71), so what a big leaf hits culls the rest of the traversal, and here a lane at a
+// big leaf would wait for the wave's big-leaf round while the others step on.  Instead a lane's first big
+// leaf is remembered the moment the lane reaches it (an inner step landing on it, a pop returning it, or
+// the big-leaf round for a lone-traversal exit), the lane steps on, and when every lane of the wave is
+// done the remembered leaves run through the ordinary big-leaf rounds (twin quads / units, leaf trees) from
+// the bound the rest of the scene left.  Priced and checked on the CPU first (tools/defer_probe.c, tests/
+// test_defer_rule.py: 0 differences from the reference order; config 4's tree leaf: the bound finite for
+// 77 % of its visits instead of 43 %).  Why the result is the reference's: the end phase in trace.
+constexpr uint32_t DEFER_NONE = 0xffffffffu, DEFER_OFF = 0xfffffffeu, DEFER_END1 = 0xfffffffdu, DEFER_END2 = 0xfffffffcu;
+// Per lane, 5 words of wave-private LDS (tree kernels keep coop_tree's 64-word compaction area first):
+// D[0] the deferred leaf's first index, or DEFER_NONE / DEFER_OFF (after a redo) / DEFER_END1 / DEFER_END2
+// (its rounds are running), D[64] its count, D[128] `closest` when it was reached, D[192] `closest` at the
+// end of the rest, D[256] the leaf's first index during END1, then the guard's bound.
+constexpr int DEFER_WORDS = 5 * 64;
+template <int MODE>
+__device__ __forceinline__ uint32_t* defer_words(uint32_t* scratch) {
+    return scratch + ((MODE & 4) ? 64 : 0) + (threadIdx.x & 63u);
+}
 
 __device__ __forceinline__ float next_up(float t) {  // the next float above t >= 0 (or -0)
     return __uint_as_float((__float_as_uint(t) & 0x7fffffffu) + 1u);
 }
-constexpr int DEFER_LDS_WORDS = 64 + 7 * 64;
 
 // Only rays and scenes inside +-2^16 defer (the ray's origin; the scene's root box, scalar loads): every
 // product of the slab and triangle tests is then finite, so no NaN distance -- whose place in the order of
-// accepts would matter -- can arise after the deferral.
-__device__ __forceinline__ bool defer_leaf(uint32_t* scratch, const float4* nodes4, const Trav& T, const Ray& R,
-                                           const Hit& h) {
-    uint32_t* D = scratch + 64 + (threadIdx.x & 63u);
-    if (D[0] != DEFER_NONE || !(h.best <= 1e30f) || !R.fast) return false;
+// accepts would matter -- can arise after the deferral.  D = the lane's words, or null: deferral off.
+__device__ __forceinline__ bool defer_leaf(uint32_t* D, const float4* nodes4, const Trav& T, const Ray& R, const Hit& h) {
+    if (!D || D[0] != DEFER_NONE || !(h.best <= 1e30f) || !R.fast) return false;
     const f4v lo = ((ConstF4)nodes4)[0], hi = ((ConstF4)nodes4)[1];
     const float sc = fmaxf(fmaxf(fmaxf(fabsf(lo.x), fabsf(lo.y)), fmaxf(fabsf(lo.z), fabsf(lo.w))),
                            fmaxf(fabsf(hi.x), fabsf(hi.y)));
     const float ro = fmaxf(fmaxf(fabsf(R.o.x), fabsf(R.o.y)), fabsf(R.o.z));
     if (!(sc < 0x1p16f && ro < 0x1p16f)) return false;
-    D[0] = T.first, D[64] = T.count, D[128] = __float_as_uint(h.best), D[192] = (uint32_t)h.kind, D[256] = h.id;
-    D[320] = __float_as_uint(h.bx), D[384] = __float_as_uint(h.by);
+    D[0] = T.first, D[64] = T.count, D[128] = __float_as_uint(h.best);
     return true;
 }
 
-// defer_leaf for a lane that has just reached a big leaf, if it is a tree leaf (lead record pf == 2)
-__device__ __forceinline__ bool defer_tree_leaf(const float4* tris, const float4* nodes4, uint32_t* scratch, const Trav& T,
-                                                const Ray& R, const Hit& h) {
-    if (!scratch) return false;
-    if (__float_as_uint(tris[3 * (size_t)T.first + 2].w) != 2u) return false;
-    return defer_leaf(scratch, nodes4, T, R, h);
-}
-
-// pop, then: a tree leaf popped as the lane's first is deferred (defer_leaf) and popping goes on
+// pop, then: a big leaf popped as the lane's first is deferred (defer_leaf) and popping goes on
 template <bool DEFER, class S>
-__device__ __forceinline__ bool pop_d(const float4* nodes4, const float4* tris, uint32_t* scratch, const S& stk, const Ray& R,
-                                      const Hit& h, Trav& T) {
+__device__ __forceinline__ bool pop_d(const float4* nodes4, uint32_t* D, const S& stk, const Ray& R, const Hit& h, Trav& T) {
     for (;;) {
         if (!pop(nodes4, stk, T.sp, R, h.best, T.first, T.count)) return false;
-        if (!DEFER || T.count <= (uint32_t)BIG || !defer_tree_leaf(tris, nodes4, scratch, T, R, h)) return true;
+        if (!DEFER || T.count <= (uint32_t)BIG || !defer_leaf(D, nodes4, T, R, h)) return true;
     }
 }
 
 // One small step of a lane at a small leaf or an inner node; false when the traversal is over.
 // (Testing a small leaf in the same step as the inner node that entered it was measured slower:
 // 22.2 vs 20.6 ms, the extra divergence costs more than the saved iterations.)
-// DEF (leaf-tree kernels, RT_TUNE bit 24 clear): a tree leaf the lane reaches as its first is deferred at once
+// DEF (deferred big leaves, D non-null): a big leaf the lane reaches as its first is deferred at once
 // (defer_leaf), so the lane steps on instead of waiting for the wave's big-leaf round.
 template <bool STATS, bool SCR = false, bool DEF = false, class S, class C>
 __device__ __forceinline__ bool small_step(const float4* nodes4, const float4* tris, const float4* spairs, const S& stk,
                                            const Ray& R, Hit& h, Trav& T, C& c, const float4* pairs = nullptr,
-                                           uint32_t* scratch = nullptr) {
+                                           uint32_t* D = nullptr) {
     if constexpr (SCR) {
         if (T.count > (uint32_t)BIG) {  // a big leaf just reached: its screen, else wait for the round
             if (!screen_leaf<STATS>(tris, pairs, R, h, T, c)) {
@@ -1147,12 +1127,12 @@ __device__ __forceinline__ bool small_step(const float4* nodes4, const float4* t
             for (uint32_t i = T.first; i < T.first + T.count; i++)
                 test_triangle<STATS>(R, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], h, c);
         }
-        if constexpr (!DEF) return pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
-    } else if (inner_step<STATS>(nodes4, stk, T.sp, R, h.best, T.first, T.count, c)) {
-        if (!DEF || T.count <= (uint32_t)BIG || !defer_tree_leaf(tris, nodes4, scratch, T, R, h)) return true;
+        return pop_d<DEF>(nodes4, D, stk, R, h, T);
     }
-    if constexpr (!DEF) return pop(nodes4, stk, T.sp, R, h.best, T.first, T.count);
-    else return pop_d<DEF>(nodes4, tris, scratch, stk, R, h, T);
+    if (inner_step<STATS>(nodes4, stk, T.sp, R, h.best, T.first, T.count, c)) {
+        if (!DEF || T.count <= (uint32_t)BIG || !defer_leaf(D, nodes4, T, R, h)) return true;
+    }
+    return pop_d<DEF>(nodes4, D, stk, R, h, T);
 }
 
 // One big-leaf round, called by all lanes of the wave in converged control flow.  `big` = the
@@ -1160,12 +1140,12 @@ __device__ __forceinline__ bool small_step(const float4* nodes4, const float4* t
 // waiting lane run it together (pairs / cooperative rounds / scalar loads); if every waiting
 // lane is at that leaf, or each lane alone otherwise (MODE: see trace).  Returns whether this
 // lane ran its leaf (it then pops; the others keep waiting).
-template <bool STATS, int MODE, bool DEFER = false, class C>
+template <bool STATS, int MODE, class C>
 __device__ __forceinline__ bool big_round(const float4* tris, const float4* pairs, const float4* quads, const float4* units,
                                           const float4* tree,
                                           const float4* ltris, const float4* flat, uint32_t* scratch, uint32_t tune,
                                           unsigned long long big, bool waiting,
-                                          const Ray& R, Hit& h, const Trav& T, C& c, const float4* nodes4 = nullptr) {
+                                          const Ray& R, Hit& h, const Trav& T, C& c) {
     if ((MODE & 4) && tree) {  // MODE bit 2: the scene has leaf trees
         // lanes at leaves with a leaf tree (mirror.h: lead record pf == 2) walk it on their own
         bool at_tree = false;
@@ -1175,23 +1155,15 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
             at_tree = __float_as_uint(lead.w) == 2u;
             root = __float_as_uint(lead.z);
         }
-        unsigned long long mt = __ballot(at_tree);
+        const unsigned long long mt = __ballot(at_tree);
         if (mt) {
-            if constexpr (DEFER) {
-                // a lane's first tree leaf is deferred to the end of its traversal (defer_leaf)
-                if (flat && (tune & 0x41000000u) == 0) {
-                    const bool dfr = at_tree && defer_leaf(scratch, nodes4, T, R, h);
-                    mt = __ballot(at_tree && !dfr);
-                    if (!mt) return at_tree;
-                }
-            }
             if (!STATS && flat && (tune & 0x40000000u) == 0)  // RT_TUNE bit 30: per-lane walk instead
             {
                 const unsigned long long tt0 = (MODE & 8) ? __builtin_amdgcn_s_memtime() : 0;
                 coop_tree<(MODE & 8) != 0>(tris, tree, ltris, flat, mt, root, R, h, T, scratch, tune, c, h.best);
                 if (MODE & 8) c.cy_tree += __builtin_amdgcn_s_memtime() - tt0;
             }
-            else if (at_tree && (mt >> (threadIdx.x & 63u)) & 1ull)
+            else if (at_tree)
                 tree_leaf<STATS>(tris, tree, ltris, root, T.first, T.count, R, h, c);
             return at_tree;
         }
@@ -1284,6 +1256,22 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
             test_triangle<STATS>(R, tris[3 * i], tris[3 * i + 1], tris[3 * i + 2], h, c);
     }
     return waiting;
+}
+
+// big_round for the lanes waiting at a big leaf, after deferring the lanes for which it is the first (D
+// non-null; lanes that reach a big leaf through the lone traversal defer here, the others at arrival).
+template <bool STATS, int MODE, class C>
+__device__ __forceinline__ bool big_round_d(const float4* nodes4, uint32_t* D, const float4* tris, const float4* pairs,
+                                            const float4* quads, const float4* units, const float4* tree,
+                                            const float4* ltris, const float4* flat, uint32_t* scratch, uint32_t tune,
+                                            unsigned long long big, bool waiting, const Ray& R, Hit& h, const Trav& T, C& c) {
+    const bool dfr = waiting && defer_leaf(D, nodes4, T, R, h);
+    if (__ballot(dfr)) {
+        waiting = waiting && !dfr;
+        big = __ballot(waiting);
+        if (!big) return dfr;
+    }
+    return big_round<STATS, MODE>(tris, pairs, quads, units, tree, ltris, flat, scratch, tune, big, waiting, R, h, T, c) || dfr;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1477,10 +1465,15 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
     // big-leaf screens (screen_leaf, MODE bit 5): split-step variants for scenes that have them
     constexpr bool scr_on = !STATS && (MODE & 16) != 0 && (MODE & 32) != 0;
     constexpr bool TIMING = (MODE & 8) != 0;
-    constexpr bool DEFER = !STATS && (MODE & 4) != 0;  // leaf-tree scenes: deferred tree leaves
-    if constexpr (DEFER) scratch[64 + (threadIdx.x & 63u)] = DEFER_NONE;
-    // deferral at arrival (small_step, pop_d): the scratch to defer into, or null when it is off
-    uint32_t* const dscr = (DEFER && tree && flat && (tune & 0x41000000u) == 0) ? scratch : nullptr;
+    // deferred big leaves (defer_leaf): production, timing and refill variants, not the screen ones; D = this
+    // lane's words, or null when deferral is off (RT_TUNE bit 24)
+#if defined(RT_DEFER_ALL)  // experiment: every kernel defers (config 2's floor leaf too)
+    constexpr bool DEFER = !STATS && (MODE & 32) == 0;
+#else  // the leaf-tree kernels (config 2's 7-wave kernel spills 53 -> 186 dwords with the deferral compiled in)
+    constexpr bool DEFER = !STATS && (MODE & 32) == 0 && (MODE & 4) != 0;
+#endif
+    uint32_t* const D = (DEFER && (tune & (1u << 24)) == 0) ? defer_words<MODE>(scratch) : nullptr;
+    if (D) D[0] = DEFER_NONE;
     unsigned long long t0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
     for (;;) {
         if constexpr ((MODE & 16) != 0) {
@@ -1524,7 +1517,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                 // exists to gather lanes per kind, which matters little when both groups are small)
                 if (!scr_on && mI && mL && nI + nL <= (uint32_t)RT_COMBINE_T) {
                     if (inner || leafs) {
-                        active = small_step<STATS, false, DEFER>(nodes4, tris, spairs, stk, R, h, T, c, nullptr, dscr);
+                        active = small_step<STATS, false, DEFER>(nodes4, tris, spairs, stk, R, h, T, c, nullptr, D);
                         if (TIMING) c.lane_work++;
                     }
                 } else
@@ -1535,7 +1528,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                         if (TIMING) c.lane_work++;
                     }
                 } else if (inner) {
-                    active = small_step<STATS, false, DEFER>(nodes4, tris, spairs, stk, R, h, T, c, nullptr, dscr);
+                    active = small_step<STATS, false, DEFER>(nodes4, tris, spairs, stk, R, h, T, c, nullptr, D);
                     if (TIMING) c.lane_work++;
                 }
 #ifdef RT_LANE_HIST
@@ -1573,74 +1566,66 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
         }
         const unsigned long long big = __ballot(active);  // every active lane waits at a big leaf
         if (!big) {
-            if constexpr (DEFER) {
-                // the deferred tree leaves, walked with the bound the rest of the traversal left
-                uint32_t* D = scratch + 64 + (threadIdx.x & 63u);
-                const uint32_t df = D[0];
-                const bool pend = df < DEFER_OFF;
-                if (__ballot(pend)) {
-                    const unsigned long long td0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
-                    const uint32_t entry = D[128];
-                    bool redo = pend && !(h.best == h.best);
-                    // a hit found after the leaf loses ties to it: the bound just above that hit
-                    const float bnd = __float_as_uint(h.best) != entry ? next_up(h.best) : h.best;
-                    Trav TD;
-                    TD.first = pend ? df : 0u, TD.count = pend ? D[64] : 0u, TD.sp = T.sp;
-                    const uint32_t root = pend ? __float_as_uint(tris[3 * (size_t)df + 2].z) : 0u;
-                    const uint32_t h1 = __float_as_uint(h.best);
-                    const unsigned long long mw = __ballot(pend && !redo);
-                    if (mw) coop_tree<TIMING, true>(tris, tree, ltris, flat, mw, root, R, h, TD, scratch, tune, c, bnd, &redo);
-                    // The rest's best hit F came after the leaf and the leaf has nothing at or below it.  The
-                    // reference walked the leaf first, and reaches F's leaf P -- and P's ancestors, whose boxes
-                    // contain P's, so their rounded slab tmin is at most tmin_P -- only if `closest` stayed above
-                    // tmin_P, i.e. if the leaf holds nothing at or below tmin_P.  tmin_P <= t_F: shown by the walk
-                    // above.  tmin_P > t_F (a rounded distance below its own box's rounded entry: a triangle on a
-                    // box face, or an ill-conditioned grazing hit): the leaf once more up to tmin_P, and the
-                    // lane redone in the reference order if that finds anything (or if F's leaf is unknown).
-                    const bool chk = pend && !redo && h1 != entry && __float_as_uint(h.best) == h1 && h.kind == 2;
-                    bool again = false;
-                    float tp = 0.0f;
-                    if (chk) {
-                        const uint32_t P = face_leaf ? face_leaf[h.id] : 0xffffffffu;
-                        if (P >= 0xfffffffeu) {
-                            redo = true;
-                        } else {
-                            float tx;
-                            slab_exact(R, ldo(nodes4, 2 * P), ldo(nodes4, 2 * P + 1), &tp, &tx);
-                            again = tp > h.best;
+            if (DEFER && D) {
+                // Every lane's rest is done: the deferred leaves' rounds, through the loop's own big-leaf round.
+                // END1 runs the leaf from the bound the rest left: just above a hit found after the leaf (the
+                // leaf came first in DFS order and wins that tie), or the hit it was entered with (strict <).
+                // When it finds nothing there, the rest's best hit F stands -- if the reference, having run the
+                // leaf first, still reaches F's leaf P: P's ancestors contain its box, so their rounded slab tmin
+                // is at most tmin_P, and it does iff the leaf holds nothing at or below tmin_P.  tmin_P <= t_F:
+                // shown by END1.  tmin_P > t_F (a rounded distance below its own box's rounded entry: a triangle
+                // on a box face, or an ill-conditioned grazing hit): END2 runs the leaf up to tmin_P, and if it
+                // finds anything the lane is redone from the root in the reference order with `closest` = the
+                // distance it had at the leaf (the leaf then accepts a hit, so the fields of the hit it had at the
+                // leaf never survive, and nothing before the leaf in DFS order lies below that distance).
+                const uint32_t st = D[0];
+                bool go = false;
+                if (st < DEFER_END2) {  // deferred: END1
+                    const uint32_t entry = D[128], h1 = __float_as_uint(h.best);
+                    D[192] = h1, D[256] = st, D[0] = DEFER_END1;  // D[256]: the leaf until END2 needs the word
+                    h.best = h1 != entry ? next_up(h.best) : h.best;
+                    T.first = st, T.count = D[64];
+                    go = true;
+                } else if (st == DEFER_END1) {
+                    const uint32_t entry = D[128], h1 = D[192];
+                    const float bnd = h1 != entry ? next_up(__uint_as_float(h1)) : __uint_as_float(h1);
+                    D[0] = DEFER_NONE;
+                    if (__float_as_uint(h.best) == __float_as_uint(bnd)) {  // nothing in the leaf at or below F
+                        h.best = __uint_as_float(h1);
+                        if (h1 != entry) {  // F came after the leaf: the guard
+                            const uint32_t P = face_leaf ? face_leaf[h.id] : 0xffffffffu;
+                            float tp = INFINITY, tx;
+                            if (P < 0xfffffffeu) slab_exact(R, ldo(nodes4, 2 * P), ldo(nodes4, 2 * P + 1), &tp, &tx);
+                            if (tp > h.best) {  // (F's leaf unknown: tp = inf, the whole leaf below the entry)
+                                const float b2 = P < 0xfffffffeu ? next_up(tp) : __uint_as_float(entry);
+                                T.first = D[256], T.count = D[64];
+                                D[256] = __float_as_uint(b2), D[0] = DEFER_END2;
+                                h.best = b2;
+                                go = true;
+                            }
                         }
                     }
-                    const unsigned long long ma = __ballot(again);
-                    if (ma) {
-                        coop_tree<TIMING, true>(tris, tree, ltris, flat, ma, root, R, h, TD, scratch, tune, c, next_up(tp),
-                                                &redo);
-                        if (again && __float_as_uint(h.best) != h1) redo = true;
-                    }
-                    if (pend) D[0] = redo ? DEFER_OFF : DEFER_NONE;
-                    if (TIMING) {
-                        c.cy_tree += __builtin_amdgcn_s_memtime() - td0;
-                        c.lane_work += pend ? 3u : 0u;
-                    }
-                    if (__ballot(redo)) {
-                        // NaN after the deferral: this lane's traversal again, from the hit at the leaf,
-                        // with deferral off (never taken for finite scenes)
-                        if (redo) {
-                            h.best = __uint_as_float(entry), h.kind = (int)D[192], h.id = D[256];
-                            h.bx = __uint_as_float(D[320]), h.by = __uint_as_float(D[384]);
-                            active = trav_begin<STATS>(nodes4, R, h, T, c);
-                        }
-                        continue;
+                } else if (st == DEFER_END2) {
+                    if (__float_as_uint(h.best) != D[256]) {  // the leaf holds a hit at or below tmin_P: redo
+                        h.best = __uint_as_float(D[128]);
+                        D[0] = DEFER_OFF;
+                        active = trav_begin<STATS>(nodes4, R, h, T, c);
+                    } else {
+                        h.best = __uint_as_float(D[192]);
+                        D[0] = DEFER_NONE;
                     }
                 }
+                if (go) active = true;
+                if (__ballot(active)) continue;
             }
             break;
         }
-        if (big_round<STATS, MODE, DEFER>(tris, pairs, quads, units, tree, ltris, flat, scratch, tune, big, active, R, h, T, c,
-                                          nodes4)) {
+        if (big_round_d<STATS, MODE>(nodes4, D, tris, pairs, quads, units, tree, ltris, flat, scratch, tune, big, active, R, h,
+                                     T, c)) {
             // a big leaf run alone (cooperative round) costs about as much as 3 small steps
             if (TIMING) c.lane_work += 3;
             if constexpr (scr_on) T.sp &= ~SCREENED;
-            active = pop_d<DEFER>(nodes4, tris, dscr, stk, R, h, T);
+            active = pop_d<DEFER>(nodes4, D, stk, R, h, T);
         }
         if (TIMING) {
             const unsigned long long t1 = __builtin_amdgcn_s_memtime();

@@ -373,7 +373,7 @@ template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
     constexpr int SL = STACK < RT_LDS_SL ? STACK : RT_LDS_SL;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
     __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
-    __shared__ uint32_t scratch_lds[(MODE & 4) ? rtfast::DEFER_LDS_WORDS : 1];  // coop_tree's compaction + deferred leaves
+    __shared__ uint32_t scratch_lds[((MODE & 4) ? 64 : 0) + rtfast::DEFER_WORDS];  // coop_tree's compaction, deferred leaves
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
     render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds, ovf}, scratch_lds);
 }
@@ -381,7 +381,7 @@ template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(5))) void render_fast_kernel_w5(RenderArgs a) {
     constexpr int SL = STACK < RT_LDS_SL ? STACK : RT_LDS_SL;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
     __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
-    __shared__ uint32_t scratch_lds[(MODE & 4) ? rtfast::DEFER_LDS_WORDS : 1];  // coop_tree's compaction + deferred leaves
+    __shared__ uint32_t scratch_lds[((MODE & 4) ? 64 : 0) + rtfast::DEFER_WORDS];  // coop_tree's compaction, deferred leaves
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
     render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds, ovf}, scratch_lds);
 }
@@ -389,7 +389,7 @@ template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(6))) void render_fast_kernel_w6(RenderArgs a) {
     constexpr int SL = STACK < RT_LDS_SL ? STACK : RT_LDS_SL;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
     __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
-    __shared__ uint32_t scratch_lds[(MODE & 4) ? rtfast::DEFER_LDS_WORDS : 1];  // coop_tree's compaction + deferred leaves
+    __shared__ uint32_t scratch_lds[((MODE & 4) ? 64 : 0) + rtfast::DEFER_WORDS];  // coop_tree's compaction, deferred leaves
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
     render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds, ovf}, scratch_lds);
 }
@@ -397,7 +397,7 @@ template <int STACK, bool STATS, int MODE>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(7))) void render_fast_kernel_w7(RenderArgs a) {
     constexpr int SL = STACK < RT_LDS_SL ? STACK : RT_LDS_SL;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
     __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
-    __shared__ uint32_t scratch_lds[(MODE & 4) ? rtfast::DEFER_LDS_WORDS : 1];  // coop_tree's compaction + deferred leaves
+    __shared__ uint32_t scratch_lds[((MODE & 4) ? 64 : 0) + rtfast::DEFER_WORDS];  // coop_tree's compaction, deferred leaves
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
     render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds, ovf}, scratch_lds);
 }

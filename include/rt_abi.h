@@ -495,9 +495,9 @@ int rt_scene_mirror_nodes(rt_scene* scene, GPUBVHNode* nodes, size_t* count);
 /* The big leaves' twin records (mirror.h quads: 28 floats each, units: 16 floats each), built on the
    host: counts first, then the arrays when the pointers are not NULL.  0 or -1. */
 int rt_scene_mirror_twins(rt_scene* scene, float* quads, size_t* quad_count, float* units, size_t* unit_count);
-/* Scenes with leaf trees: the leaf of every face (mirror.h face_leaf: the private node index, 0xffffffff
-   in no leaf, 0xfffffffe in two), which the deferred tree leaves' guard reads (rt_fast.h).  *count
-   receives the face count (0 for scenes without leaf trees); leaf (may be NULL) the table.  0 or -1. */
+/* Scenes with big leaves: the leaf of every face (mirror.h face_leaf: the private node index, 0xffffffff
+   in no leaf, 0xfffffffe in two), which the deferred leaves' guard reads (rt_fast.h).  *count receives
+   the face count (0 for scenes without big leaves); leaf (may be NULL) the table.  0 or -1. */
 int rt_scene_mirror_face_leaf(rt_scene* scene, uint32_t* leaf, size_t* count);
 
 /* Test hook: the private mirror built on the host from raw reference arrays (the foreign-scene path,

@@ -296,17 +296,18 @@ def test_overlapping_big_leaves_get_no_twins():
 
 
 def test_face_leaf_table():
-    """The deferred tree leaves' guard table (mirror.h face_leaf, rt_fast.h): for a scene with leaf trees,
-    every face maps to the private node of the one leaf that holds it -- whose box is then the box the
-    reference tests before that face (main_raytracing.cu:43-71) -- checked against the reference arrays
-    walked independently; scenes without leaf trees carry no table."""
+    """The deferred leaves' guard table (mirror.h face_leaf, rt_fast.h): for a scene with big leaves, every
+    face maps to the private node of the one leaf that holds it -- whose box is then the box the reference
+    tests before that face (main_raytracing.cu:43-71) -- checked against the reference arrays walked
+    independently."""
     rt = T.load_rt()
+    for which in ("bunny", "bunny4"):
+        _check_face_leaf(rt, which)
+
+
+def _check_face_leaf(rt, which):
     s = rt.Scene()
-    s.setup("bunny")
-    s.build()
-    assert s.mirror_face_leaf().size == 0
-    s = rt.Scene()
-    s.setup("bunny4")
+    s.setup(which)
     s.build()
     fl = s.mirror_face_leaf()
     arrays = s.host_arrays()
