@@ -226,6 +226,23 @@ def test_refill_equals_full(rt, refill, mapped):
     assert np.array_equal(rng.cpu().numpy(), rng_full)
 
 
+def test_refill_with_leaf_trees_equals_full(rt):
+    """The refill kernels of a leaf-tree scene (the 4-bunny frame: cooperative tree walks, deferred tree
+    leaves and their end phase inside the refill loop) equal the plain render bit for bit."""
+    w, h, spp, bounces = 640, 360, 2, 4
+    full, rng_full = full_frames(rt, w, h, spp, bounces, 1, "bunny4")
+    s = scene(rt, w, h, "bunny4")
+    mine = torch.arange(rt.sharding.tiles_total(w, h), dtype=torch.int32, device="cuda")
+    rng = rt.alloc_rng(w * h)
+    rt.init_rng_states(rng, w, h, T.SEED)
+    s.upload(rng.data_ptr())
+    a, b = rt.alloc_surface(w, h), rt.alloc_surface(w, h)
+    rt.render(s, a, b, w, h, spp, bounces, 0, tile_list=mine, refill_lanes=16)
+    torch.cuda.synchronize()
+    assert np.array_equal(rt.surface_view(a, w).cpu().numpy().view(np.uint32), full.view(np.uint32))
+    assert np.array_equal(rng.cpu().numpy(), rng_full)
+
+
 @pytest.mark.parametrize("which", ["bunny", "bunny4"])
 def test_one_pixel_waves_equal_full(rt, which):
     """A lane map with ONE pixel per wave: every traversal runs through the lone-ray path
