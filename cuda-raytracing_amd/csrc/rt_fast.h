@@ -864,11 +864,10 @@ __device__ __forceinline__ f3 bcast3(f3 v, int lane) {
     return rtm::mk(bcast(v.x, lane), bcast(v.y, lane), bcast(v.z, lane));
 }
 
-// bnd_l: the lane's starting bound (its `closest`).
 template <bool TIMING, class C>
 __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree, const float4* ltris, const float4* flat,
                                           unsigned long long m, uint32_t root_l, const Ray& R, Hit& h, const Trav& T,
-                                          uint32_t* scratch, uint32_t tune, C& c, float bnd_l) {
+                                          uint32_t* scratch, uint32_t tune, C& c) {
     const uint32_t lane = threadIdx.x & 63u;
     // RT_TUNE bit 31: visit surviving subtrees nearest box first (costs more than it saves here:
     // 117 vs 111 ms on the 4-bunny frame), else in tree order
@@ -887,7 +886,7 @@ __device__ __forceinline__ void coop_tree(const float4* tris, const float4* tree
         B.d = B.nd, B.r = B.nd;  // unused by cluster_cull / leaf_candidate
         B.fast = __builtin_amdgcn_readlane(R.fast ? 1 : 0, r) != 0;
         const f3 rnd = bcast3(rnd_l, r);
-        const float best = bcast(bnd_l, r);
+        const float best = bcast(h.best, r);
         const f4v K2 = ((ConstF4)(tree + 4 * (size_t)root))[2];
         const f4v KR = ((ConstF4)(tree + 4 * (size_t)root))[3];
         const uint32_t cb = __float_as_uint(K2.x), nc = __float_as_uint(K2.y), kb = __float_as_uint(K2.z),
@@ -1160,7 +1159,7 @@ __device__ __forceinline__ bool big_round(const float4* tris, const float4* pair
             if (!STATS && flat && (tune & 0x40000000u) == 0)  // RT_TUNE bit 30: per-lane walk instead
             {
                 const unsigned long long tt0 = (MODE & 8) ? __builtin_amdgcn_s_memtime() : 0;
-                coop_tree<(MODE & 8) != 0>(tris, tree, ltris, flat, mt, root, R, h, T, scratch, tune, c, h.best);
+                coop_tree<(MODE & 8) != 0>(tris, tree, ltris, flat, mt, root, R, h, T, scratch, tune, c);
                 if (MODE & 8) c.cy_tree += __builtin_amdgcn_s_memtime() - tt0;
             }
             else if (at_tree)

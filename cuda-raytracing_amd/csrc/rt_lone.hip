@@ -113,7 +113,7 @@ __device__ __forceinline__ void lone_leaf(const RenderArgs& a, const float4* tri
     const uint32_t pf = __float_as_uint(lead.w), po = __float_as_uint(lead.z);
     if ((MODE & 4) && pf == 2u && a.tree && a.flat) {
         Trav T{f0, c0, 0};
-        coop_tree<false>(tris, a.tree, a.ltris, a.flat, 1ull, po, R, h, T, scratch, a.tune, c, h.best);
+        coop_tree<false>(tris, a.tree, a.ltris, a.flat, 1ull, po, R, h, T, scratch, a.tune, c);
     } else if ((pf & 1u) && a.pairs) {  // pf 3: a screen record precedes the pairs (mirror.h)
         coop_leaf(tris, a.pairs + 5 * (size_t)po, 1ull, f0, c0, R, h);
     } else {
