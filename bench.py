@@ -545,6 +545,7 @@ def production_counts(t):
            "wave_big_iters": t["wave_big_iters"]}
     if t["cycles_tree_cut"]:
         out["cycles_frac"]["tree_walk"] = round(t["cycles_tree_cut"] / tot, 4)
+        out["defer_end2"], out["defer_redo"] = t["defer_end2"], t["defer_redo"]
     return out
 
 

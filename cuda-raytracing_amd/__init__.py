@@ -33,7 +33,7 @@ STAT_NAMES = ("segments", "nodes", "tri_tests", "tri_accepts", "sphere_accepts",
               "wave_small_iters", "lane_small", "wave_big_tris", "lane_big_tris", "wave_segment_iters",
               "lane_segments", "tree_nodes", "tree_tri_tests", "cycles_small", "cycles_big", "cycles_total",
               "rounds_coop", "rounds_shared", "coop_rays", "cycles_tree_clusters", "cycles_tree_tris",
-              "big_tests", "twin_decided", "twin_tests", "wave_big_iters", None, None, None, None)
+              "big_tests", "twin_decided", "twin_tests", "wave_big_iters", "defer_end2", "defer_redo", None, None)
 STAT_COUNT = len(STAT_NAMES)  # RT_STAT_COUNT (include/rt_abi.h): per-wave records of RT_TUNE bit 11 follow
 SCENES = {"bunny": 0, "bunny4": 1, "plane1m": 2}
 

@@ -93,13 +93,11 @@ def disassemble(obj):
                               capture_output=True, text=True).stdout
 
 
-def exec_narrowing_hazards(dis):
-    """Vector instructions that run under an exec mask narrowed without a save (`s_and_b64 exec, exec, c`)
-    in the blocks its execz branch skips to, before the parent's `s_or_b64 exec, exec, s` restores the
-    mask: the lanes turned off never run them, although in the thread-level CFG the register allocator
-    sees every lane of the parent region passes through that block (rt_fast_body.h RT_FAST_FAMILY).
-    `dis` is llvm-objdump output; returns [(kernel, narrowing address, [instructions])]."""
-    base, ins = {}, []  # symbol -> address; (address, text, branch target or None, kernel)
+def parse_disassembly(dis):
+    """llvm-objdump text -> ({symbol: address}, [(address, text, (symbol, offset) branch target or None,
+    kernel)]).  The format it relies on: `ADDR <sym>:` symbol lines and instruction lines ending in
+    `// ADDR: encoding` with `<sym+0xOFF>` on branches (tests/test_build_guard.py pins it)."""
+    base, ins = {}, []
     kernel = None
     for ln in dis.split("\n"):
         m = re.match(r"^([0-9a-f]+) <(\S+)>:$", ln)
@@ -111,6 +109,16 @@ def exec_narrowing_hazards(dis):
         if m:
             tgt = (m.group(3), int(m.group(4), 16)) if m.group(3) else None
             ins.append((int(m.group(2), 16), m.group(1), tgt, kernel))
+    return base, ins
+
+
+def exec_narrowing_hazards(dis):
+    """Vector instructions that run under an exec mask narrowed without a save (`s_and_b64 exec, exec, c`)
+    in the blocks its execz branch skips to, before the parent's `s_or_b64 exec, exec, s` restores the
+    mask: the lanes turned off never run them, although in the thread-level CFG the register allocator
+    sees every lane of the parent region passes through that block (rt_fast_body.h RT_FAST_FAMILY).
+    `dis` is llvm-objdump output; returns [(kernel, narrowing address, [instructions])]."""
+    base, ins = parse_disassembly(dis)
     at = {a: i for i, (a, _, _, _) in enumerate(ins)}
     out = []
     for i, (addr, text, _, k) in enumerate(ins):
@@ -141,11 +149,24 @@ def exec_narrowing_hazards(dis):
 def check_exec_narrowing(objs):
     """Build guard: no HIP object may carry exec_narrowing_hazards (the miscompile of round 4's 6-wave
     kernel).  Raises RuntimeError naming the kernel and the instructions."""
-    problems = []
+    problems, flagged = [], []
     for obj in objs:
-        for k, addr, bad in exec_narrowing_hazards(disassemble(obj)):
+        dis = disassemble(obj)
+        if dis and not parse_disassembly(dis)[1]:
+            # device code present but nothing parsed: the objdump format changed, the guard would pass blind
+            problems.append(f"{os.path.basename(obj)}: device code but no instruction parsed (llvm-objdump format?)")
+            flagged.append(obj)
+            continue
+        for k, addr, bad in exec_narrowing_hazards(dis):
             problems.append(f"{os.path.basename(obj)}: {k} at 0x{addr:x}: " + "; ".join(bad[:4]))
+            flagged.append(obj)
     if problems:
+        # drop the flagged objects and their command records so the next build recompiles and re-checks
+        # them instead of linking them as up to date
+        for obj in set(flagged):
+            for f in (obj, obj + ".cmd"):
+                if os.path.exists(f):
+                    os.remove(f)
         raise RuntimeError("exec narrowed without a save with vector code behind it (tools/exec_narrow_scan.py, "
                            "rt_fast_body.h RT_FAST_FAMILY):\n  " + "\n  ".join(problems))
 
@@ -186,14 +207,18 @@ def build_product(force=False):
     exp_jobs = [_hip_job(src) for src in EXP_SOURCES]
     changed = _compile(jobs + exp_jobs, force)
     objs = [o for o, _ in jobs]
-    if changed:
+    eobjs = [o for o, _ in exp_jobs]
+    relink = changed or not _newer(LIB, objs)
+    relink_exp = changed or not _newer(EXP_LIB, eobjs + [LIB])
+    if relink or relink_exp:
+        # guard every object about to be linked, whether or not this build compiled it (a flagged object
+        # is deleted, so it can never be linked by a later build as up to date)
         check_exec_narrowing([o for o, _ in jobs + exp_jobs if o.endswith(".hip.o")])
-    if changed or not _newer(LIB, objs):
+    if relink:
         tmp = LIB + ".tmp"
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-L/opt/rocm/lib", "-lrccl", "-o", tmp])
         os.replace(tmp, LIB)
-    eobjs = [o for o, _ in exp_jobs]
-    if changed or not _newer(EXP_LIB, eobjs + [LIB]):
+    if relink_exp:
         tmp = EXP_LIB + ".tmp"
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *eobjs, "-L", PKG, "-l:librt_hip.so",
               "-Wl,-rpath,$ORIGIN", "-Wl,--no-undefined", "-o", tmp])

@@ -83,6 +83,7 @@ struct Counters {
     unsigned long long cy_tcl = 0, cy_ttri = 0, cy_tree = 0;  // timing: leaf-tree cluster / triangle rounds, whole walk
     uint32_t lane_work = 0;  // timing: this lane's own traversal steps (+3 per big leaf), rt_render_params.lane_cost
     unsigned long long big_tests = 0, tw_test = 0, tw_dec = 0, big_iters = 0;  // timing: big-leaf work by twins
+    uint32_t end2 = 0, redo = 0;  // timing: this lane's deferral guard walks and redos (rt_fast.h trace)
 };
 
 __device__ __forceinline__ rtm::f3 ld3(const float* p) { return rtm::f3{p[0], p[1], p[2]}; }

@@ -1600,6 +1600,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                                 T.first = D[256], T.count = D[64];
                                 D[256] = __float_as_uint(b2), D[0] = DEFER_END2;
                                 h.best = b2;
+                                if (TIMING) c.end2++;
                                 go = true;
                             }
                         }
@@ -1608,6 +1609,7 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                     if (__float_as_uint(h.best) != D[256]) {  // the leaf holds a hit at or below tmin_P: redo
                         h.best = __uint_as_float(D[128]);
                         D[0] = DEFER_OFF;
+                        if (TIMING) c.redo++;
                         active = trav_begin<STATS>(nodes4, R, h, T, c);
                     } else {
                         h.best = __uint_as_float(D[192]);

@@ -174,6 +174,10 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
     // process sharing the GPU (the shader-cycle counter s_memtime is not)
     const unsigned long long rt_start = (a.wave_clock || ((MODE & 8) && (a.tune & 2048u))) ? __builtin_amdgcn_s_memrealtime() : 0;
 
+#ifdef RT_LIVE_HIST
+    unsigned long long lh_t = 0;
+    uint32_t lh_n = 0;
+#endif
     for (;;) {
         if (!drained) {
             const unsigned long long idle = __ballot(!pixel && !path);
@@ -246,6 +250,20 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
                 if ((MODE & 8) && a.lane_cost) a.lane_cost[slot] = c.lane_work + (uint32_t)c.seg;
             }
         }
+#ifdef RT_LIVE_HIST  // diagnostic build (tools/lane_hist.sh LIVE=1): segment-loop wave cycles by live pixels
+        if (MODE & 8) {
+            const unsigned long long tn = __builtin_amdgcn_s_memtime();
+            if (lh_t) {
+                const unsigned long long dt = tn - lh_t;
+                c.ktest += lh_n <= 8u ? dt : 0ull;                    // 1-8 live pixels
+                c.ktri += (lh_n > 8u && lh_n <= 16u) ? dt : 0ull;     // 9-16
+                c.cy_tcl += (lh_n > 16u && lh_n <= 32u) ? dt : 0ull;  // 17-32
+                c.cy_ttri += dt;                                      // every segment-loop iteration
+            }
+            lh_t = tn;
+            lh_n = (uint32_t)__popcll(__ballot(pixel || path));
+        }
+#endif
         if (!__ballot(path)) {
             if (drained) break;
             continue;  // every lane idle: refill at the top
@@ -304,11 +322,11 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
             lane_max = o > lane_max ? o : lane_max;
         }
     unsigned long long lane_sum = c.l_small;  // the wave's lane-steps in small-step iterations (timing frame)
-    unsigned long long big_sum[3] = {c.big_tests, c.tw_dec, c.tw_test};  // per lane -> the wave's
+    unsigned long long big_sum[5] = {c.big_tests, c.tw_dec, c.tw_test, c.end2, c.redo};  // per lane -> the wave's
     if ((MODE & 8) && a.stats)
         for (int off = 32; off > 0; off >>= 1) {
             lane_sum += __shfl_xor(lane_sum, off);
-            for (int k = 0; k < 3; k++) big_sum[k] += __shfl_xor(big_sum[k], off);
+            for (int k = 0; k < 5; k++) big_sum[k] += __shfl_xor(big_sum[k], off);
         }
     if ((MODE & 8) && a.stats && threadIdx.x == 0) {  // timing frame: per-wave phase clocks
         atomicAdd(a.stats + RT_STAT_CYCLES_SMALL, c.cy_small);
@@ -323,6 +341,8 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
         atomicAdd(a.stats + RT_STAT_TWIN_DECIDED, big_sum[1]);
         atomicAdd(a.stats + RT_STAT_TWIN_TESTS, big_sum[2]);
         atomicAdd(a.stats + RT_STAT_WAVE_BIG_ITERS, c.big_iters);
+        atomicAdd(a.stats + RT_STAT_DEFER_END2, big_sum[3]);
+        atomicAdd(a.stats + RT_STAT_DEFER_REDO, big_sum[4]);
         // cooperative leaf-tree walk (wave-level): rays, subtree + cluster tests, triangle rounds
         atomicAdd(a.stats + RT_STAT_TREE_NODES, c.ktest);
         atomicAdd(a.stats + RT_STAT_TREE_TRI_TESTS, c.ktri);

@@ -841,6 +841,9 @@ extern "C" int rt_render(const rt_render_params* p, const GPUScene* scene, void*
     auto trav = [&](const RenderArgs& x) {  // the arguments as they stand at launch, traversal nodes
         RenderArgs f = x;
         f.nodes = trav_nodes;
+        // the face -> leaf table holds private-array node indices: with the reference's array (bit 27) the
+        // deferral guard must not look them up there -- without a table it walks the leaf up to the entry
+        if (trav_nodes != (const GPUBVHNode*)mir.nodes) f.face_leaf = nullptr;
         return f;
     };
     hipError_t e;

@@ -261,6 +261,9 @@ enum {
     RT_STAT_TWIN_DECIDED = 25,      /* twins rejected from their partner's values without a test (rt_fast.h twin_rejected) */
     RT_STAT_TWIN_TESTS = 26,        /* twins tested themselves (too close to call, or a hit) */
     RT_STAT_WAVE_BIG_ITERS = 27,    /* wave iterations of those tests (shared-leaf quads, cooperative unit chunks) */
+    /* timing frames of the leaf-tree kernels: deferred big leaves (rt_fast.h defer_leaf) */
+    RT_STAT_DEFER_END2 = 28,        /* guard walks (END2: the leaf re-run up to tmin of the hit's own leaf) */
+    RT_STAT_DEFER_REDO = 29,        /* lanes redone from the root after END2 found a hit */
     RT_STAT_COUNT = 32
 };
 

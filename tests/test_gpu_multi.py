@@ -478,25 +478,44 @@ def test_big_leaf_screens_equal_plain(rt, wps):
     assert np.array_equal(res[0][1], res[1 << 28][1])
 
 
-@pytest.mark.parametrize("wps", [5, 6, 7])
-def test_deferred_tree_leaves_equal_reference_order(rt, wps):
+@pytest.mark.parametrize("wps,base", [(5, 0), (6, 0), (7, 0), (5, 1 << 27)])
+def test_deferred_tree_leaves_equal_reference_order(rt, wps, base):
     """Deferred leaf trees (rt_fast.h defer_leaf: a lane's first tree leaf walked at the end of its
     traversal, with the bound the rest of the scene left and ties decided by DFS order) render the
     4-bunny frame and RNG states bit for bit as the walk at the leaf (RT_TUNE bit 24), at every
-    occupancy; the full-frame oracle fixture of config 4 (test_gpu_fullframe.py) covers the default."""
+    occupancy; the full-frame oracle fixture of config 4 (test_gpu_fullframe.py) covers the default.
+    base = bit 27 traverses the reference's node array, where the guard's face -> leaf table (private
+    node indices) must not be used (rt_render drops it: ADVICE round 5)."""
     w, h, spp, bounces = 256, 144, 4, 6
     res = {}
+    if base:
+        rt.load_experimental()
     for tune in (0, 1 << 24):  # bit 24: deferral off
         s = scene(rt, w, h, "bunny4")
         rng = rt.alloc_rng(w * h)
         rt.init_rng_states(rng, w, h, T.SEED)
         s.upload(rng.data_ptr())
         a, b = rt.alloc_surface(w, h), rt.alloc_surface(w, h)
-        rt.render(s, a, b, w, h, spp, bounces, 0, waves_per_simd=wps, tune=tune)
+        rt.render(s, a, b, w, h, spp, bounces, 0, waves_per_simd=wps, tune=tune | base)
         torch.cuda.synchronize()
         res[tune] = (rt.surface_view(a, w).cpu().numpy().copy(), rng.cpu().numpy().copy())
     assert np.array_equal(res[0][0].view(np.uint32), res[1 << 24][0].view(np.uint32))
     assert np.array_equal(res[0][1], res[1 << 24][1])
+    if wps == 5 and not base:
+        # the guard's second walk (END2) runs on this frame: the timing variant counts it (ADVICE round 5);
+        # its redo branch is rarer still (0 of 250,700 sampled config-4 segments, tests/test_defer_rule.py)
+        s = scene(rt, w, h, "bunny4")
+        rng = rt.alloc_rng(w * h)
+        rt.init_rng_states(rng, w, h, T.SEED)
+        s.upload(rng.data_ptr())
+        a, b = rt.alloc_surface(w, h), rt.alloc_surface(w, h)
+        st = torch.zeros(rt.STAT_COUNT, dtype=torch.int64, device="cuda")
+        rt.render(s, a, b, w, h, spp, bounces, 0, waves_per_simd=wps, stats=st, tune=256)
+        torch.cuda.synchronize()
+        t = dict(zip(rt.STAT_NAMES, st.cpu().tolist()))
+        print("deferral guard: END2 walks", t["defer_end2"], "redos", t["defer_redo"])
+        assert t["defer_end2"] > 0
+        assert np.array_equal(rt.surface_view(a, w).cpu().numpy().view(np.uint32), res[0][0].view(np.uint32))
 
 
 def test_lone_and_lane_overlap_is_caught(rt):
