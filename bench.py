@@ -71,6 +71,13 @@ PMC_PASSES = [
     ["FETCH_SIZE"],
     ["WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"],
 ]
+# optional pass (round 6): the issue side -- LDS instructions and bank-conflict cycles, scalar-memory instructions,
+# the CU's one scalar ALU (quad-cycles), and where wave cycles go (issue stall / waiting / issuing); a failure
+# here leaves the required passes' numbers in place
+PMC_PASSES_OPTIONAL = [
+    ["SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_INSTS_SMEM", "SQ_INST_CYCLES_SALU", "SQ_ACTIVE_INST_SCA",
+     "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY"],
+]
 
 
 def algorithmic_bytes(stats, sphere_count, pixels):
@@ -270,7 +277,9 @@ def pmc_pass(args, out_dir, timeout_s=150):
     if rocprof is None:
         return None, "rocprofv3 not found"
     counters, kernel, durations = {}, None, []
-    for i, cs in enumerate(PMC_PASSES):
+    optional_error = None
+    for i, cs in enumerate(PMC_PASSES + PMC_PASSES_OPTIONAL):
+        optional = i >= len(PMC_PASSES)
         d = os.path.join(out_dir, f"pass{i}")
         cmd = [rocprof, "--kernel-trace", "--pmc", *cs, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
                sys.executable, os.path.abspath(__file__), "--pmc-child", "--config", args.config,
@@ -289,23 +298,33 @@ def pmc_pass(args, out_dir, timeout_s=150):
             r = subprocess.run(cmd, cwd=tempfile.gettempdir(), capture_output=True, text=True, timeout=timeout_s,
                                env=dict(os.environ, TMPDIR=tempfile.gettempdir()))
         except subprocess.TimeoutExpired:
+            if optional:
+                optional_error = f"pass {i} timed out"
+                break
             return None, f"pass {i} timed out"
         os.makedirs(d, exist_ok=True)
         with open(os.path.join(d, "child.log"), "w") as fh:
             fh.write(r.stdout + "\n---- stderr ----\n" + r.stderr)
         if r.returncode != 0:
             err = [l for l in r.stderr.splitlines() if "Error" in l or "error" in l or "Traceback" in l]
-            return None, f"pass {i} exit {r.returncode}: {' | '.join(err[-3:])[-400:]}"
+            msg = f"pass {i} exit {r.returncode}: {' | '.join(err[-3:])[-400:]}"
+            if optional:
+                optional_error = msg
+                break
+            return None, msg
         vals, k, dur = read_pmc_pass(d)
         kernel = k or kernel
         if i == 0:
             durations = dur
         if not vals:
+            if optional:
+                optional_error = f"pass {i}: no render_fast_kernel rows"
+                break
             return None, f"pass {i}: no render_fast_kernel rows"
         # rows are per dispatch and counter (summed over XCDs by rocprofv3's csv); mean per dispatch
         for c, v in vals.items():
             counters[c] = sum(v) / len(v)
-    return {"counters": counters, "kernel": kernel,
+    return {"counters": counters, "kernel": kernel, "optional_error": optional_error,
             "profiled_kernel_s": float(np.mean(durations)) if durations else None}, None
 
 
@@ -337,6 +356,18 @@ def roofline(pmc, kern_s, bytes_alg, err=None):
     out["hbm"] = {"bytes_per_launch": hbm, "achieved_gbs": round(hbm / kern_s / 1e9, 1), "peak_gbs": HBM_PEAK_GBS,
                   "frac": round(hbm / kern_s / 1e9 / HBM_PEAK_GBS, 4),
                   "l2_hit_rate": round(c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 4)}
+    if "SQ_INSTS_LDS" in c:  # the optional issue-side pass
+        wc = max(1.0, c["SQ_WAVE_CYCLES"])
+        out["issue"] = {"lds_instructions_per_launch": int(c["SQ_INSTS_LDS"]),
+                        "lds_bank_conflict_cycles": int(c["SQ_LDS_BANK_CONFLICT"]),
+                        "smem_instructions_per_launch": int(c["SQ_INSTS_SMEM"]),
+                        "salu_wave_cycles": int(4 * c["SQ_INST_CYCLES_SALU"]),  # waves' cycles in SALU instructions
+                        # per-SE aggregates over the waves (SQ_WAVE_CYCLES' basis): where a wave's cycles go
+                        "wave_frac_issuing": round(c["SQ_ACTIVE_INST_ANY"] / wc, 4),
+                        "wave_frac_issue_stalled": round(c["SQ_WAIT_INST_ANY"] / wc, 4),
+                        "wave_frac_waiting": round(c["SQ_WAIT_ANY"] / wc, 4)}
+    elif pmc.get("optional_error"):
+        out["issue"] = {"error": pmc["optional_error"]}
     out["pmc_counters"] = {k: round(v, 1) for k, v in sorted(c.items())}
     return out
 

@@ -154,22 +154,26 @@ __device__ __forceinline__ float4 ldc(ConstF4 p, uint32_t i) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
-// The traversal stack of one lane: node indices, the first SL entries in LDS (lane stride WAVE),
-// deeper ones in a private per-lane array (scratch memory).  Deep stacks are rare -- no ray of a
-// config-2 frame goes past 15 entries -- so a 16-entry LDS stack (4 KB per wave) costs nothing
+// The traversal stack of one lane: node indices, the first SL entries in LDS (lane stride WGL, the
+// workgroup's lanes), deeper ones in a private per-lane array (scratch memory).  Deep stacks are rare -- no
+// ray of a config-2 frame goes past 15 entries -- so a 16-entry LDS stack (4 KB per wave) costs nothing
 // and leaves registers, not LDS, as the occupancy limit.
-template <int SL>
+template <int SL, int WGL = WAVE>
 struct Stack {
     static constexpr int LDS_ENTRIES = SL;
+    static constexpr int LANES = WGL;  // lanes sharing the LDS rows (one wave, or a wave pair: trace)
     // A lane's stack pointer is ENCODED as the byte offset of its next entry from lane 0's entry 0:
-    // sp = 4 * lane + 256 * depth (entry i of lane l at lds0[l + i * WAVE]).  The LDS address of an entry is
-    // then lds0 + sp, one wave-uniform base and the pointer the lane already holds: no per-lane column
+    // sp = 4 * column + 4 WGL * depth (entry i of column l at lds0[l + i * WGL]).  The LDS address of an entry
+    // is then lds0 + sp, one uniform base and the pointer the lane already holds: no per-lane column
     // address to keep live beside it (the 7-wave build spilled that address and reloaded it on every pop).
-    uint32_t* lds0;  // lane 0's entry 0 (wave-uniform)
+    // The column is the workgroup lane that started the ray; a ray handed to another lane of the workgroup
+    // (wave pairs, trace) keeps its column and so its entries.
+    uint32_t* lds0;  // column 0's entry 0 (workgroup-uniform)
     uint32_t* ovf;   // this lane's entries SL, SL + 1, ...
-    static __device__ __forceinline__ int depth(int sp) { return sp >> 8; }
-    static __device__ __forceinline__ int empty(int lane) { return 4 * lane; }  // sp of an empty stack
-    static constexpr int STEP = 4 * WAVE;                                         // sp per entry
+    static constexpr int STEP = 4 * WGL;  // sp per entry
+    static __device__ __forceinline__ int depth(int sp) { return sp / STEP; }
+    static __device__ __forceinline__ int column(int sp) { return (sp & (STEP - 1)) >> 2; }
+    static __device__ __forceinline__ int empty(int col) { return 4 * col; }  // sp of an empty stack
     __device__ __forceinline__ uint32_t* at(int sp) const {
         return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(lds0) + sp);
     }
@@ -182,7 +186,13 @@ struct Stack {
         if (__builtin_expect(depth(sp) >= SL, 0)) return ovf[depth(sp) - SL];
         return *at(sp);
     }
+    // the LDS word of entry sp, or the lane's word of the pad row SL (STACK_PAD_ROWS) past the LDS entries:
+    // a store that need not happen (an entry above the top) goes there without a branch
+    __device__ __forceinline__ uint32_t* at_clamped(int sp) const {
+        return at(sp < SL * STEP ? sp : (sp & (STEP - 1)) + SL * STEP);
+    }
 };
+constexpr int STACK_PAD_ROWS = 1;  // LDS rows allocated past a Stack's SL entries (at_clamped)
 
 // Pop stack entries until one passes `tmin < closest` (the reference's pop-time test).  An
 // entry is a node index (lane stride WAVE in LDS); tmin is recomputed from the node with the same
@@ -190,22 +200,21 @@ struct Stack {
 template <class S>
 __device__ __forceinline__ bool pop(const float4* nodes4, const S& stk, int& sp, const Ray& R, float best,
                                     uint32_t& first, uint32_t& count) {
-    while (sp >= S::STEP) {  // depth > 0 (sp = 4 * lane + 256 * depth)
+    // One rare branch per entry: the approximate test runs for every ray (R.fast false only routes the entry
+    // to the IEEE test) and the entry is read from LDS unless it lies in the overflow part (round 6: VALU and
+    // SALU per launch -1.4 % each against the same loop with the R.fast, UNSURE and overflow branches apart)
+    while (sp >= S::STEP) {
         sp -= S::STEP;
-        const uint32_t idx = stk.get(sp);
+        uint32_t idx = *stk.at_clamped(sp);
+        if (__builtin_expect(S::depth(sp) >= S::LDS_ENTRIES, 0)) idx = stk.ovf[S::depth(sp) - S::LDS_ENTRIES];
         const float4 lo = ldo(nodes4, 2 * idx), hi = ldo(nodes4, 2 * idx + 1);
-        int cl = UNSURE;
         float te, tx;
-        if (R.fast) {
-            slab_approx(R, lo, hi, &te, &tx);
-            cl = classify_lt(te, best);
-        }
-        bool pass;
-        if (cl == UNSURE) {
+        slab_approx(R, lo, hi, &te, &tx);
+        const int cl = classify_lt(te, best);
+        bool pass = cl == YES;
+        if (!R.fast || cl == UNSURE) {
             slab_exact(R, lo, hi, &te, &tx);
             pass = te < best;
-        } else {
-            pass = cl == YES;
         }
         if (pass) {
             first = __float_as_uint(hi.z), count = __float_as_uint(hi.w);
@@ -224,6 +233,38 @@ __device__ __forceinline__ bool inner_step(const float4* nodes4, const S& stk, i
     const float4 l0 = ldo(nodes4, 2 * first), l1 = ldo(nodes4, 2 * first + 1);
     const float4 r0 = ldo(nodes4, 2 * first + 2), r1 = ldo(nodes4, 2 * first + 3);
     if (STATS) c.node += 2;
+#if defined(RT_BF_STEP) || defined(RT_BF_INNER)
+    // The same decisions with one rare branch: every decision the reference's order needs here (left and
+    // right pass, the right's `tmin < closest`, and the left's when the right fails) from the approximate
+    // slabs when none is too close to call, else all from the IEEE slabs (each approximate decision that
+    // is made equals the exact one, so any mix gives the reference's).  The left index is stored whether
+    // or not it is pushed (the entry at sp is above the top) and the stack pointer moves only on a push.
+    {
+        float tl, tlx, tr, trx;
+        slab_approx(R, l0, l1, &tl, &tlx);
+        slab_approx(R, r0, r1, &tr, &trx);
+        const int okl = classify_ok(tl, tlx), okr = classify_ok(tr, trx);
+        const int rlt = classify_lt(tr, best), llt = classify_lt(tl, best);
+        bool goR = okr == YES && rlt == YES;
+        bool okL = okl == YES;
+        bool goL = !goR && okL && llt == YES;
+        const bool sure = R.fast && okl != UNSURE && okr != UNSURE && (okr == NO || rlt != UNSURE) &&
+                          (goR || okl == NO || llt != UNSURE);
+        if (!sure) {
+            slab_exact(R, l0, l1, &tl, &tlx);
+            slab_exact(R, r0, r1, &tr, &trx);
+            okL = tlx >= tl && tlx > 0.0f;
+            goR = trx >= tr && trx > 0.0f && tr < best;
+            goL = !goR && okL && tl < best;
+        }
+        const bool push = goR && okL;
+        *stk.at_clamped(sp) = first;
+        if (__builtin_expect(push && S::depth(sp) >= S::LDS_ENTRIES, 0)) stk.ovf[S::depth(sp) - S::LDS_ENTRIES] = first;
+        sp += push ? S::STEP : 0;
+        first = __float_as_uint(goR ? r1.z : l1.z), count = __float_as_uint(goR ? r1.w : l1.w);
+        return goR || goL;
+    }
+#endif
     float tl = 0.0f, tlx = 0.0f, tr = 0.0f, trx = 0.0f;
     int okl = UNSURE, okr = UNSURE, rlt = UNSURE;
     if (R.fast) {
@@ -1023,7 +1064,7 @@ __device__ __forceinline__ bool trav_begin(const float4* nodes4, const Ray& R, c
     if (STATS) c.node++;
     float tmin, tmax;
     slab_exact(R, lo, hi, &tmin, &tmax);
-    T.first = __float_as_uint(hi.z), T.count = __float_as_uint(hi.w), T.sp = (int)(threadIdx.x & 63u) * 4;  // empty
+    T.first = __float_as_uint(hi.z), T.count = __float_as_uint(hi.w), T.sp = (int)threadIdx.x * 4;  // empty, own column
     return tmax >= tmin && tmin < h.best && tmax > 0.0f;
 }
 
@@ -1294,12 +1335,15 @@ __device__ __forceinline__ bool big_round_d(const float4* nodes4, uint32_t* D, c
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t bcastu(uint32_t v, int lane) { return (uint32_t)__builtin_amdgcn_readlane((int)v, lane); }
 
-template <int SL>
-__device__ __forceinline__ void lone_traverse(const float4* nodes4, const float4* tris, const Stack<SL>& stk, int r,
+template <class S>
+__device__ __forceinline__ void lone_traverse(const float4* nodes4, const float4* tris, const S& stk, int r,
                                               const Ray& R, Hit& h, Trav& T, bool& active) {
+    constexpr int SL = S::LDS_ENTRIES;
     const int lane = (int)(threadIdx.x & 63u);
-    uint32_t* const col = stk.lds0 + r;  // lane r's LDS stack column
-    int sp = Stack<SL>::depth((int)bcastu((uint32_t)T.sp, r));  // lane r's depth
+    const int sp0 = (int)bcastu((uint32_t)T.sp, r);
+    const int rc = S::column(sp0);           // lane r's ray's LDS stack column (its own lane, or its donor's)
+    uint32_t* const col = stk.lds0 + rc;
+    int sp = S::depth(sp0);  // lane r's depth
     uint32_t cf = bcastu(T.first, r), cc = bcastu(T.count, r);
     Ray U;  // the lone ray, wave-uniform
     U.o = bcast3(R.o, r), U.d = bcast3(R.d, r), U.nd = bcast3(R.nd, r), U.r = bcast3(R.r, r);
@@ -1314,7 +1358,7 @@ __device__ __forceinline__ void lone_traverse(const float4* nodes4, const float4
     float e_tmin = 0.0f;
     bool e_exact = false;
     if (lane < sp) {
-        e_idx = col[lane * WAVE];
+        e_idx = col[lane * S::LANES];
         const float4 lo = nodes4[2 * e_idx], hi = nodes4[2 * e_idx + 1];
         float tx;
         if (U.fast) {
@@ -1434,18 +1478,96 @@ __device__ __forceinline__ void lone_traverse(const float4* nodes4, const float4
     }
     // back to lane r: its traversal state, hit, and (when it stops at a big leaf) its stack
     if (lane == r) {
-        T.first = cf, T.count = cc, T.sp = Stack<SL>::empty(r) + sp * Stack<SL>::STEP;
+        T.first = cf, T.count = cc, T.sp = S::empty(rc) + sp * S::STEP;
         h.best = best, h.kind = kind, h.id = id, h.bx = bx, h.by = by;
         active = !done;
     }
     if (!done) {
-        if (lane < sp && lane < SL) col[lane * WAVE] = e_idx;
+        if (lane < sp && lane < SL) col[lane * S::LANES] = e_idx;
         for (int j = SL; j < sp; j++) {
             const uint32_t v = bcastu(e_idx, j);
-            if (lane == r) stk.put(Stack<SL>::empty(r) + j * Stack<SL>::STEP, v);
+            if (lane == r) stk.put(S::empty(rc) + j * S::STEP, v);
         }
     }
 }
+
+// ---------------------------------------------------------------------------------------
+// Wave pairs (RT_PAIR = K, experiment: two waves per workgroup).  A wave's traversal ends with a tail: a
+// few lanes still stepping while the rest wait (config 2, 7 waves per SIMD: small-step iterations with 1-4
+// active lanes are 13 % of wave cycles, lone-lane traversals 4 %), and every one of those iterations is
+// issued for 64 lanes.  Here a wave whose small phase is down to <= K rays (no lane waiting at a big leaf)
+// hands them to the other wave of its workgroup, which runs them in its FREE lanes -- lanes with no segment
+// this call (their pixel is done), whose ray, hit and traversal registers are dead -- beside its own rays;
+// the donor sleeps until their hits come back.  Exact by construction: a ray's traversal is the same
+// sequence of steps whichever lane runs it; its LDS stack stays where it is (Stack: the stack pointer
+// carries the ray's column), only rays whose entries all live in LDS move, and an adopted ray finishes where
+// it was adopted.  The exchange goes through an LDS mailbox: word 0 the protocol word, then field f of ray k
+// at 1 + f PAIR_K + k of the posting wave's region (21 fields: o, d, nd, 1/d, fast, hit, first, count, sp), the hit coming back in its own
+// fields.  Protocol word: bit w = wave w is in trace and may be handed rays, bits 8 + 8w.. = its free lanes,
+// bits 24-25 = phase (EMPTY, POSTED, ADOPTED, DONE), bit 26 = the posting wave, bits 27-31 = ray count.  Only
+// lane 0 of a wave changes it (compare-and-swap); the posting wave waits for DONE, the other one adopts a
+// POSTED hand-over before it may leave trace, so nothing is left behind and nothing waits on a wave that
+// cannot answer.
+// ---------------------------------------------------------------------------------------
+#if defined(RT_PAIR)
+constexpr int PAIR_K = RT_PAIR;
+constexpr uint32_t PH_EMPTY = 0u, PH_POSTED = 1u, PH_ADOPTED = 2u, PH_DONE = 3u;
+constexpr int PAIR_FIELDS = 21;
+constexpr int PAIR_MAIL_WORDS = 1 + 2 * PAIR_FIELDS * PAIR_K;  // the protocol word + one region per posting wave
+// the region wave w posts its rays in (and gets their hits back in): a wave never writes into the region of a
+// hand-over it did not post
+__device__ __forceinline__ uint32_t* pair_region(uint32_t* mail, uint32_t w) { return mail + w * PAIR_FIELDS * PAIR_K; }
+__device__ __forceinline__ uint32_t pair_phase(uint32_t st) { return (st >> 24) & 3u; }
+__device__ __forceinline__ uint32_t pair_free(uint32_t st, uint32_t w) { return (st >> (8u + 8u * w)) & 127u; }
+__device__ __forceinline__ uint32_t pair_load(uint32_t* mail) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)__hip_atomic_load(mail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+// lane 0 replaces the protocol word by f(old) while f accepts old; returns (wave-uniform) whether it did
+template <class F>
+__device__ __forceinline__ bool pair_update(uint32_t* mail, F f) {
+    int ok = 0;
+    if ((threadIdx.x & 63u) == 0) {
+        uint32_t old = __hip_atomic_load(mail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP), nw;
+        while (f(old, nw)) {
+            if (__hip_atomic_compare_exchange_strong(mail, &old, nw, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                ok = 1;
+                break;
+            }
+        }
+    }
+    return __builtin_amdgcn_readfirstlane(ok) != 0;
+}
+__device__ __forceinline__ void pair_put_hit(uint32_t* mail, int k, const Hit& h) {
+    uint32_t* m = mail + 1 + k;
+    m[13 * PAIR_K] = __float_as_uint(h.best), m[14 * PAIR_K] = (uint32_t)h.kind, m[15 * PAIR_K] = h.id;
+    m[16 * PAIR_K] = __float_as_uint(h.bx), m[17 * PAIR_K] = __float_as_uint(h.by);
+}
+__device__ __forceinline__ void pair_get_hit(const uint32_t* mail, int k, Hit& h) {
+    const uint32_t* m = mail + 1 + k;
+    h.best = __uint_as_float(m[13 * PAIR_K]), h.kind = (int)m[14 * PAIR_K], h.id = m[15 * PAIR_K];
+    h.bx = __uint_as_float(m[16 * PAIR_K]), h.by = __uint_as_float(m[17 * PAIR_K]);
+}
+__device__ __forceinline__ void pair_put_ray(uint32_t* mail, int k, const Ray& R, const Hit& h, const Trav& T) {
+    uint32_t* m = mail + 1 + k;
+    const float v[12] = {R.o.x, R.o.y, R.o.z, R.d.x, R.d.y, R.d.z, R.nd.x, R.nd.y, R.nd.z, R.r.x, R.r.y, R.r.z};
+    for (int f = 0; f < 12; f++) m[f * PAIR_K] = __float_as_uint(v[f]);
+    m[12 * PAIR_K] = R.fast ? 1u : 0u;
+    pair_put_hit(mail, k, h);
+    m[18 * PAIR_K] = T.first, m[19 * PAIR_K] = T.count, m[20 * PAIR_K] = (uint32_t)T.sp;
+}
+__device__ __forceinline__ void pair_get_ray(const uint32_t* mail, int k, Ray& R, Hit& h, Trav& T) {
+    const uint32_t* m = mail + 1 + k;
+    R.o = rtm::mk(__uint_as_float(m[0]), __uint_as_float(m[PAIR_K]), __uint_as_float(m[2 * PAIR_K]));
+    R.d = rtm::mk(__uint_as_float(m[3 * PAIR_K]), __uint_as_float(m[4 * PAIR_K]), __uint_as_float(m[5 * PAIR_K]));
+    R.nd = rtm::mk(__uint_as_float(m[6 * PAIR_K]), __uint_as_float(m[7 * PAIR_K]), __uint_as_float(m[8 * PAIR_K]));
+    R.r = rtm::mk(__uint_as_float(m[9 * PAIR_K]), __uint_as_float(m[10 * PAIR_K]), __uint_as_float(m[11 * PAIR_K]));
+    R.fast = m[12 * PAIR_K] != 0u;
+    pair_get_hit(mail, k, h);
+    T.first = m[18 * PAIR_K], T.count = m[19 * PAIR_K], T.sp = (int)m[20 * PAIR_K];
+}
+#endif
 
 // BVHRayHit for one lane (`live` = the lane has a segment to trace), every lane of the wave
 // calling.  Small steps run while any lane has one; big leaves wait until every lane is done
@@ -1457,10 +1579,43 @@ template <bool STATS, int MODE, class S, class C>
 __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, const float4* pairs,
                                       const float4* tree, const float4* ltris, const float4* flat,
                                       const float4* spairs, uint32_t tune, const S& stk, uint32_t* scratch,
-                                      const Ray& R, Hit& h, bool live, C& c, const float4* quads = nullptr,
-                                      const float4* units = nullptr, const uint32_t* face_leaf = nullptr) {
+                                      Ray& R, Hit& h, bool live, C& c, const float4* quads = nullptr,
+                                      const float4* units = nullptr, const uint32_t* face_leaf = nullptr,
+                                      uint32_t* mail = nullptr) {
     Trav T{0, 0, 0};
     bool active = live && trav_begin<STATS>(nodes4, R, h, T, c);
+#if defined(RT_PAIR)
+    // wave pairs (above): the production split-step kernels without leaf trees, screens or refill
+#if defined(RT_PAIR_NOEXCH)  // A/B: the pair workgroups without the exchange
+    constexpr bool PAIR = false;
+#else
+    constexpr bool PAIR = !STATS && (MODE & 8) == 0 && (MODE & 4) == 0 && (MODE & 16) != 0 && (MODE & 32) == 0 &&
+                          (MODE & 64) == 0;
+#endif
+#ifndef RT_PAIR_EVERY
+#define RT_PAIR_EVERY 1  // iterations between two looks at the mailbox
+#endif
+    uint32_t pair_tick = 0;
+    const uint32_t pw = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // this wave of the pair
+    const uint32_t po = 1u - pw;
+    int adopted = -1;         // mail slot of the other wave's ray this lane runs, or -1
+    uint32_t n_adopted = 0;   // rays adopted (wave-uniform)
+    if (PAIR && mail) {       // in trace: may be handed up to (free lanes) rays
+        const uint32_t nfree = min((uint32_t)__popcll(__ballot(!live)), 127u);
+        pair_update(mail, [&](uint32_t o, uint32_t& nw) {
+            nw = (o & ~(127u << (8u + 8u * pw))) | (1u << pw) | (nfree << (8u + 8u * pw));
+            return true;
+        });
+    }
+    auto pair_publish = [&]() {  // every adopted ray done: their hits back, DONE
+        if (adopted >= 0) pair_put_hit(pair_region(mail, po), adopted, h);
+        adopted = -1, n_adopted = 0;
+        pair_update(mail, [](uint32_t o, uint32_t& nw) {
+            nw = (o & ~(3u << 24)) | (PH_DONE << 24);
+            return true;
+        });
+    };
+#endif
     // big-leaf screens (screen_leaf, MODE bit 5): split-step variants for scenes that have them
     constexpr bool scr_on = !STATS && (MODE & 16) != 0 && (MODE & 32) != 0;
     constexpr bool TIMING = (MODE & 8) != 0;
@@ -1475,6 +1630,57 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
     if (D) D[0] = DEFER_NONE;
     unsigned long long t0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
     for (;;) {
+#if defined(RT_PAIR)
+        if (PAIR && mail && (RT_PAIR_EVERY == 1 || (++pair_tick % RT_PAIR_EVERY) == 0)) {
+            const uint32_t st = pair_load(mail);
+            const uint32_t ph = pair_phase(st);
+            if (ph == PH_POSTED && ((st >> 26) & 1u) != pw) {  // rays handed to this wave: free lanes take them
+                const uint32_t n = st >> 27;
+                const bool fr = !live && adopted < 0;
+                const unsigned long long fm = __ballot(fr);
+                const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+                if (fr && k < n) {
+                    pair_get_ray(pair_region(mail, po), (int)k, R, h, T);
+                    adopted = (int)k;
+                    active = true;
+                }
+                n_adopted = n;
+                pair_update(mail, [](uint32_t o, uint32_t& nw) {
+                    nw = (o & ~(3u << 24)) | (PH_ADOPTED << 24);
+                    return true;
+                });
+                continue;
+            }
+            if (n_adopted && !__ballot(adopted >= 0 && active)) pair_publish();
+            const bool mine = active && T.count <= (uint32_t)BIG;  // this wave's small-phase rays
+            const unsigned long long mS = __ballot(mine);
+            const uint32_t nS = (uint32_t)__popcll(mS);
+            if (!n_adopted && ph == PH_EMPTY && nS && nS <= (uint32_t)PAIR_K && mS == __ballot(active) &&
+                ((st >> po) & 1u) && pair_free(st, po) >= nS && !__ballot(mine && S::depth(T.sp) > S::LDS_ENTRIES)) {
+                const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(mS >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mS, 0u));
+                if (mine) pair_put_ray(pair_region(mail, pw), (int)k, R, h, T);
+                if (pair_update(mail, [&](uint32_t o, uint32_t& nw) {
+                        if (pair_phase(o) != PH_EMPTY || !((o >> po) & 1u) || pair_free(o, po) < nS) return false;
+                        nw = (o & 0x00ffffffu) | (PH_POSTED << 24) | (pw << 26) | (nS << 27);
+                        return true;
+                    })) {
+                    // (bounded: a protocol error renders wrong pixels -- the parity tests catch those -- instead of
+                    // hanging the device; ~2^22 sleeps is far beyond any traversal)
+                    for (uint32_t spin = 0; pair_phase(pair_load(mail)) != PH_DONE && spin < (1u << 22); spin++)
+                        __builtin_amdgcn_s_sleep(2);
+                    if (mine) {
+                        pair_get_hit(pair_region(mail, pw), (int)k, h);
+                        active = false;
+                    }
+                    pair_update(mail, [](uint32_t o, uint32_t& nw) {
+                        nw = o & 0x00ffffffu;  // EMPTY
+                        return true;
+                    });
+                    continue;
+                }
+            }
+        }
+#endif
         if constexpr ((MODE & 16) != 0) {
             // split small steps: inner-node steps and small-leaf steps run in separate wave
             // iterations (a lane at a small leaf waits until at least half as many lanes are at
@@ -1619,6 +1825,18 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                 if (go) active = true;
                 if (__ballot(active)) continue;
             }
+#if defined(RT_PAIR)
+            if (PAIR && mail) {
+                if (n_adopted) pair_publish();
+                // leave trace: no more rays for this wave, unless a hand-over to it is already POSTED
+                if (!pair_update(mail, [&](uint32_t o, uint32_t& nw) {
+                        if (pair_phase(o) == PH_POSTED && ((o >> 26) & 1u) != pw) return false;
+                        nw = o & ~(1u << pw) & ~(127u << (8u + 8u * pw));
+                        return true;
+                    }))
+                    continue;  // adopt it first
+            }
+#endif
             break;
         }
         if (big_round_d<STATS, MODE>(nodes4, D, tris, pairs, quads, units, tree, ltris, flat, scratch, tune, big, active, R, h,

@@ -114,10 +114,17 @@ __device__ __forceinline__ int xcd_block(uint32_t tune) {
 #ifndef RT_LDS_SL
 #define RT_LDS_SL 16  // stack entries in LDS (4 KB per wave)
 #endif
+#if defined(RT_PAIR)  // experiment (rt_fast.h wave pairs): two waves per workgroup, tails handed over
+constexpr int WG_WAVES = 2;
+#else
+constexpr int WG_WAVES = 1;
+#endif
+constexpr int WGL = WG_WAVES * WAVE;  // lanes per workgroup (the LDS stack's column count)
 
 template <int STACK, bool STATS, int MODE>
-__device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfast::Stack<(STACK < RT_LDS_SL ? STACK : RT_LDS_SL)>& stk,
-                                                 uint32_t* const scratch) {
+__device__ __forceinline__ void render_fast_body(const RenderArgs& a,
+                                                 const rtfast::Stack<(STACK < RT_LDS_SL ? STACK : RT_LDS_SL), WGL>& stk,
+                                                 uint32_t* const scratch, uint32_t* const mail = nullptr) {
     if (a.gate && *a.gate != a.gate_value) return;  // foreign scenes: the other tracer renders this frame
     const float4* nodes4 = reinterpret_cast<const float4*>(a.nodes);
     const float4* tris = reinterpret_cast<const float4*>(a.tris);
@@ -144,13 +151,15 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
     };
     // entry i of the launch's lane order: the lane map, or slot i (wave i / 64 = 8x8 sub-tile)
     auto bind_entry = [&](long long i) {
-        const long long s = a.lane_slots ? (long long)a.lane_slots[i] : i;
+        const long long s = (WG_WAVES > 1 && i >= a.entry_count) ? -1 : a.lane_slots ? (long long)a.lane_slots[i] : i;
         const bool ok = s >= 0 && s < a.slot_count;  // a bad map entry renders nothing
         bind(ok ? (int)(s >> 8) : -1, (int)(s & 255));
     };
     // one 64-lane workgroup per 8x8 sub-tile: tile k = lb / 4, sub-tile lb % 4
-    const int lb = xcd_block(a.tune);
-    bind_entry((long long)lb * WAVE + threadIdx.x);
+    // (wave pairs: the two waves of workgroup g take sub-tiles 2g, 2g + 1)
+    const int lane = (int)(threadIdx.x & 63u);
+    const int lb = xcd_block(a.tune) * WG_WAVES + (WG_WAVES > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0);
+    bind_entry((long long)lb * WAVE + lane);
     if (a.lane_slots && lb < a.priority_waves) __builtin_amdgcn_s_setprio(3);  // the frame's long waves
     // Refill (rt_render_params.refill_lanes): the grid holds only as many waves as fit the GPU at
     // once; entries [grid x 64, entries) form a queue, and a wave whose idle lanes reach
@@ -159,7 +168,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
     // Waves that start less than half full (split waves of a lane plan) are not refilled.
     constexpr bool REFILL = (MODE & 64) != 0;  // refill is compiled into its own kernel variants only
     bool drained = !REFILL || a.queue_head == nullptr || __popcll(__ballot(pixel)) < 32;
-    const long long qbase = (long long)gridDim.x * WAVE;
+    const long long qbase = (long long)gridDim.x * WGL;
     Counters c;
     const rtm::f3 cam_o = ld3(a.cam.origin), cam_h = ld3(a.cam.horizontal), cam_v = ld3(a.cam.vertical),
                   cam_ll = ld3(a.cam.lower_left_corner);
@@ -185,7 +194,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
             if (ni && (ni >= (uint32_t)a.refill_lanes || !__ballot(path))) {
                 const int lead = __ffsll((long long)idle) - 1;
                 unsigned long long base = 0;
-                if ((int)threadIdx.x == lead) base = atomicAdd(a.queue_head, (unsigned long long)ni);
+                if (lane == lead) base = atomicAdd(a.queue_head, (unsigned long long)ni);
                 base = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(base >> 32), lead) << 32) |
                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)base, lead);
                 const long long qn = a.entry_count - qbase;
@@ -292,9 +301,9 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
                 }
             }
         }
-        const rtfast::Ray R = rtfast::make_ray(ro, rd, nd, scene_fast);
+        rtfast::Ray R = rtfast::make_ray(ro, rd, nd, scene_fast);
         rtfast::trace<STATS, MODE>(nodes4, tris, a.pairs, a.tree, a.ltris, a.flat, a.spairs, a.tune, stk, scratch, R, h,
-                                   path, c, a.quads, a.units, a.face_leaf);
+                                   path, c, a.quads, a.units, a.face_leaf, mail);
         if (!path) continue;
 
         bool end = shade_segment<STATS>(a, h, ro, rd, nd, rng, color, thr, c);
@@ -314,7 +323,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
         if ((threadIdx.x & 63) == 0) atomicAdd(a.seg_counter, v);
     }
     // per-wave cost for cost-aware shard plans (rt_render_params.wave_clock; one store per wave)
-    if (a.wave_clock && threadIdx.x == 0) a.wave_clock[lb] = __builtin_amdgcn_s_memrealtime() - rt_start;
+    if (a.wave_clock && lane == 0) a.wave_clock[lb] = __builtin_amdgcn_s_memrealtime() - rt_start;
     unsigned long long lane_max = c.l_small;  // the busiest lane's small steps (timing frame)
     if (MODE & 8)
         for (int off = 32; off > 0; off >>= 1) {
@@ -328,7 +337,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
             lane_sum += __shfl_xor(lane_sum, off);
             for (int k = 0; k < 5; k++) big_sum[k] += __shfl_xor(big_sum[k], off);
         }
-    if ((MODE & 8) && a.stats && threadIdx.x == 0) {  // timing frame: per-wave phase clocks
+    if ((MODE & 8) && a.stats && lane == 0) {  // timing frame: per-wave phase clocks
         atomicAdd(a.stats + RT_STAT_CYCLES_SMALL, c.cy_small);
         atomicAdd(a.stats + RT_STAT_CYCLES_BIG, c.cy_big);
         atomicAdd(a.stats + RT_STAT_CYCLES_TOTAL, __builtin_amdgcn_s_memtime() - t_start);
@@ -353,7 +362,7 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
         atomicAdd(a.stats + RT_STAT_CYCLES_TREE_TRIS, c.cy_ttri);
         // RT_TUNE bit 11: per-wave clocks (start, end) after the counters, for load-balance analysis
         if (a.tune & 2048u) {
-            unsigned long long* w = a.stats + RT_STAT_COUNT + 8 * (size_t)blockIdx.x;
+            unsigned long long* w = a.stats + RT_STAT_COUNT + 8 * (size_t)lb;
             w[0] = rt_start;  // 100 MHz device clock (one time base across waves)
             w[1] = __builtin_amdgcn_s_memrealtime();
             w[2] = c.cy_small;
@@ -389,37 +398,51 @@ __device__ __forceinline__ void render_fast_body(const RenderArgs& a, const rtfa
 // The production kernel.  The _w5 / _w6 / _w7 variants ask the compiler for 5 / 6 / 7 waves per
 // SIMD (fewer registers, more spilled) -- an occupancy / spill trade-off (RT_TUNE bits 9-10:
 // 0 = _w5, the default; 1 = unconstrained; 2 = _w6; 3 = _w7).
+#if defined(RT_PAIR)  // the pair's mailbox (rt_fast.h), cleared before either wave can use it
+#define RT_PAIR_MAIL                                                \
+    __shared__ uint32_t pair_mail[rtfast::PAIR_MAIL_WORDS];        \
+    if (threadIdx.x == 0) pair_mail[0] = 0u;                        \
+    __syncthreads();
+#define RT_PAIR_MAIL_ARG pair_mail
+#else
+#define RT_PAIR_MAIL
+#define RT_PAIR_MAIL_ARG nullptr
+#endif
 template <int STACK, bool STATS, int MODE>
-__global__ __launch_bounds__(WAVE) void render_fast_kernel(RenderArgs a) {
+__global__ __launch_bounds__(WGL) void render_fast_kernel(RenderArgs a) {
     constexpr int SL = STACK < RT_LDS_SL ? STACK : RT_LDS_SL;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
-    __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
+    __shared__ uint32_t stack_lds[(SL + rtfast::STACK_PAD_ROWS) * WGL];  // one word per entry (rt_fast.h pop)
     __shared__ uint32_t scratch_lds[((MODE & 4) ? 64 : 0) + rtfast::DEFER_WORDS];  // coop_tree's compaction, deferred leaves
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
-    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds, ovf}, scratch_lds);
+    RT_PAIR_MAIL
+    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL, WGL>{stack_lds, ovf}, scratch_lds, RT_PAIR_MAIL_ARG);
 }
 template <int STACK, bool STATS, int MODE>
-__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(5))) void render_fast_kernel_w5(RenderArgs a) {
+__global__ __launch_bounds__(WGL) __attribute__((amdgpu_waves_per_eu(5))) void render_fast_kernel_w5(RenderArgs a) {
     constexpr int SL = STACK < RT_LDS_SL ? STACK : RT_LDS_SL;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
-    __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
+    __shared__ uint32_t stack_lds[(SL + rtfast::STACK_PAD_ROWS) * WGL];  // one word per entry (rt_fast.h pop)
     __shared__ uint32_t scratch_lds[((MODE & 4) ? 64 : 0) + rtfast::DEFER_WORDS];  // coop_tree's compaction, deferred leaves
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
-    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds, ovf}, scratch_lds);
+    RT_PAIR_MAIL
+    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL, WGL>{stack_lds, ovf}, scratch_lds, RT_PAIR_MAIL_ARG);
 }
 template <int STACK, bool STATS, int MODE>
-__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(6))) void render_fast_kernel_w6(RenderArgs a) {
+__global__ __launch_bounds__(WGL) __attribute__((amdgpu_waves_per_eu(6))) void render_fast_kernel_w6(RenderArgs a) {
     constexpr int SL = STACK < RT_LDS_SL ? STACK : RT_LDS_SL;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
-    __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
+    __shared__ uint32_t stack_lds[(SL + rtfast::STACK_PAD_ROWS) * WGL];  // one word per entry (rt_fast.h pop)
     __shared__ uint32_t scratch_lds[((MODE & 4) ? 64 : 0) + rtfast::DEFER_WORDS];  // coop_tree's compaction, deferred leaves
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
-    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds, ovf}, scratch_lds);
+    RT_PAIR_MAIL
+    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL, WGL>{stack_lds, ovf}, scratch_lds, RT_PAIR_MAIL_ARG);
 }
 template <int STACK, bool STATS, int MODE>
-__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(7))) void render_fast_kernel_w7(RenderArgs a) {
+__global__ __launch_bounds__(WGL) __attribute__((amdgpu_waves_per_eu(7))) void render_fast_kernel_w7(RenderArgs a) {
     constexpr int SL = STACK < RT_LDS_SL ? STACK : RT_LDS_SL;  // LDS entries; deeper ones in `ovf` (rt_fast.h Stack)
-    __shared__ uint32_t stack_lds[SL * WAVE];  // one word per entry (rt_fast.h pop)
+    __shared__ uint32_t stack_lds[(SL + rtfast::STACK_PAD_ROWS) * WGL];  // one word per entry (rt_fast.h pop)
     __shared__ uint32_t scratch_lds[((MODE & 4) ? 64 : 0) + rtfast::DEFER_WORDS];  // coop_tree's compaction, deferred leaves
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
-    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL>{stack_lds, ovf}, scratch_lds);
+    RT_PAIR_MAIL
+    render_fast_body<STACK, STATS, MODE>(a, rtfast::Stack<SL, WGL>{stack_lds, ovf}, scratch_lds, RT_PAIR_MAIL_ARG);
 }
 
 // Waves of `kernel` the device holds at once (refill launches size their grid to it).
@@ -468,7 +491,7 @@ hipError_t launch_grid(K kernel, const RenderArgs& args, int waves, bool refill,
             res = std::min(res, cap * 4 * cus);  // the residency cap holds fewer
         if (res > 0) grid = std::min(waves, res);
     }
-    hipLaunchKernelGGL(kernel, dim3(grid), dim3(WAVE), lds, stream, args);
+    hipLaunchKernelGGL(kernel, dim3((grid + WG_WAVES - 1) / WG_WAVES), dim3(WGL), lds, stream, args);
     return hipGetLastError();
 }
 

@@ -252,7 +252,7 @@ __device__ __forceinline__ void wf_trace_body(const RenderArgs& a, const WfBuf& 
     const rtfast::f4v root_hi = ((rtfast::ConstF4)a.nodes)[1];
     const uint32_t root_first = __float_as_uint(root_hi.z), root_count = __float_as_uint(root_hi.w);
     constexpr int SL = STACK < 16 ? STACK : 16;
-    __shared__ uint32_t stack_lds[SL * WAVE];
+    __shared__ uint32_t stack_lds[(SL + rtfast::STACK_PAD_ROWS) * WAVE];
     __shared__ uint32_t scratch_lds[(MODE & 4) ? 64 : 1];
     uint32_t ovf[STACK > SL ? STACK - SL : 1];
     const rtfast::Stack<SL> stk{stack_lds, ovf};

@@ -41,7 +41,7 @@ def threads():
     return bench.usable_cpus()
 
 
-def render_gpu(rt, which, w, h, spp, bounces, tracer="fast"):
+def render_gpu(rt, which, w, h, spp, bounces, tracer="fast", wps=0):
     s = rt.Scene()
     s.setup(which)
     s.set_viewport(w, h)
@@ -49,7 +49,7 @@ def render_gpu(rt, which, w, h, spp, bounces, tracer="fast"):
     rt.init_rng_states(rng, w, h, T.SEED)
     s.upload(rng.data_ptr())
     a, b = rt.alloc_surface(w, h), rt.alloc_surface(w, h)
-    rt.render(s, a, b, w, h, spp, bounces, tracer=tracer)
+    rt.render(s, a, b, w, h, spp, bounces, tracer=tracer, waves_per_simd=wps)
     torch.cuda.synchronize()
     return rt.surface_view(a, w).cpu().numpy().copy(), rng.view(-1, 12)[:, :6].cpu().numpy().view(np.uint32).copy()
 
@@ -253,19 +253,19 @@ def _row_hashes(a):
     return [hashlib.sha256(np.ascontiguousarray(r).tobytes()).hexdigest()[:16] for r in a]
 
 
-@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg4"])
-def test_full_frame_matches_oracle_fixture(rt, cfg):
+@pytest.mark.parametrize("cfg,wps", [("cfg2", 0), ("cfg2", 7), ("cfg3", 0), ("cfg4", 0)])
+def test_full_frame_matches_oracle_fixture(rt, cfg, wps):
     """The whole frame of configs 2, 3 (3840x2160 64 spp) and 4 (the 4-bunny scene) against the CPU oracle's
     own full frame: tools/make_fullframe_golden.py rendered each once with oracle/rt_oracle.c (minutes of CPU
     per config, too long for this box) and tests/golden/fullframe_oracle.json keeps a SHA-256 of every row of
     the float32 frame and of the final RNG states (data only).  The production kernel's frame (default launch:
-    plain tile order, 5 waves per SIMD) must hash equal row for row -- bit-exact, every pixel and every final
-    RNG state; a mismatch names the first rows."""
+    plain tile order, 5 waves per SIMD; config 2 also at 7, the build its benchmark runs) must hash equal row for
+    row -- bit-exact, every pixel and every final RNG state; a mismatch names the first rows."""
     db = json.load(open(os.path.join(T.GOLDEN, "fullframe_oracle.json")))
     if cfg not in db:
         pytest.skip(f"no oracle fixture for {cfg} (tools/make_fullframe_golden.py {cfg})")
     g = db[cfg]
-    img, st = render_gpu(rt, g["scene"], g["width"], g["height"], g["spp"], g["bounces"])
+    img, st = render_gpu(rt, g["scene"], g["width"], g["height"], g["spp"], g["bounces"], wps=wps)
     img = img.reshape(g["height"], g["width"], 4)
     rows = _row_hashes(img)
     rng_rows = _row_hashes(st.reshape(g["height"], g["width"], 6))
@@ -273,6 +273,7 @@ def test_full_frame_matches_oracle_fixture(rt, cfg):
     bad_rng = [y for y, (a, b) in enumerate(zip(rng_rows, g["rng_rows"])) if a != b]
     with open(SUMMARY, "a") as fh:
         fh.write(json.dumps({"test": f"{cfg} full frame vs the oracle's full frame (row hashes, tests/golden/fullframe_oracle.json)",
+                             "waves_per_simd": wps or 5,
                              "values": int(img.size), "rows": len(rows), "differing_rows": len(bad),
                              "differing_rng_rows": len(bad_rng), "nan_values": int(np.isnan(img).sum()),
                              "oracle_nan_values": g["nan_values"]}) + "\n")
