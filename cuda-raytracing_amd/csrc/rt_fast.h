@@ -233,38 +233,6 @@ __device__ __forceinline__ bool inner_step(const float4* nodes4, const S& stk, i
     const float4 l0 = ldo(nodes4, 2 * first), l1 = ldo(nodes4, 2 * first + 1);
     const float4 r0 = ldo(nodes4, 2 * first + 2), r1 = ldo(nodes4, 2 * first + 3);
     if (STATS) c.node += 2;
-#if defined(RT_BF_STEP) || defined(RT_BF_INNER)
-    // The same decisions with one rare branch: every decision the reference's order needs here (left and
-    // right pass, the right's `tmin < closest`, and the left's when the right fails) from the approximate
-    // slabs when none is too close to call, else all from the IEEE slabs (each approximate decision that
-    // is made equals the exact one, so any mix gives the reference's).  The left index is stored whether
-    // or not it is pushed (the entry at sp is above the top) and the stack pointer moves only on a push.
-    {
-        float tl, tlx, tr, trx;
-        slab_approx(R, l0, l1, &tl, &tlx);
-        slab_approx(R, r0, r1, &tr, &trx);
-        const int okl = classify_ok(tl, tlx), okr = classify_ok(tr, trx);
-        const int rlt = classify_lt(tr, best), llt = classify_lt(tl, best);
-        bool goR = okr == YES && rlt == YES;
-        bool okL = okl == YES;
-        bool goL = !goR && okL && llt == YES;
-        const bool sure = R.fast && okl != UNSURE && okr != UNSURE && (okr == NO || rlt != UNSURE) &&
-                          (goR || okl == NO || llt != UNSURE);
-        if (!sure) {
-            slab_exact(R, l0, l1, &tl, &tlx);
-            slab_exact(R, r0, r1, &tr, &trx);
-            okL = tlx >= tl && tlx > 0.0f;
-            goR = trx >= tr && trx > 0.0f && tr < best;
-            goL = !goR && okL && tl < best;
-        }
-        const bool push = goR && okL;
-        *stk.at_clamped(sp) = first;
-        if (__builtin_expect(push && S::depth(sp) >= S::LDS_ENTRIES, 0)) stk.ovf[S::depth(sp) - S::LDS_ENTRIES] = first;
-        sp += push ? S::STEP : 0;
-        first = __float_as_uint(goR ? r1.z : l1.z), count = __float_as_uint(goR ? r1.w : l1.w);
-        return goR || goL;
-    }
-#endif
     float tl = 0.0f, tlx = 0.0f, tr = 0.0f, trx = 0.0f;
     int okl = UNSURE, okr = UNSURE, rlt = UNSURE;
     if (R.fast) {
