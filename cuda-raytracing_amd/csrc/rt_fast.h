@@ -1664,7 +1664,10 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
                     // one lane left in the small phase: the whole wave runs its DFS (lone_traverse),
                     // when its stack lives in LDS (RT_TUNE bit 26 turns this off); a lane that must
                     // screen a big leaf first takes an ordinary step
-                    if (nI + nL == 1 && (tune & (1u << 26)) == 0) {
+#ifndef RT_LONE_MAX
+#define RT_LONE_MAX 1  // most small-phase lanes for which the wave runs one of them as a lone ray
+#endif
+                    if (nI + nL <= (uint32_t)RT_LONE_MAX && (tune & (1u << 26)) == 0) {
                         const int r = __ffsll((long long)(mI | mL)) - 1;
                         if (S::depth(__builtin_amdgcn_readlane(T.sp, r)) <= S::LDS_ENTRIES &&
                             (!scr_on || (uint32_t)__builtin_amdgcn_readlane((int)T.count, r) <= (uint32_t)BIG)) {
