@@ -276,6 +276,7 @@ def pmc_pass(args, out_dir, timeout_s=150):
     rocprof = shutil.which("rocprofv3")
     if rocprof is None:
         return None, "rocprofv3 not found"
+    out_dir = os.path.abspath(out_dir)  # the child runs in the temp directory
     counters, kernel, durations = {}, None, []
     optional_error = None
     for i, cs in enumerate(PMC_PASSES + PMC_PASSES_OPTIONAL):
@@ -847,8 +848,12 @@ def run(args):
             gather_host_ms[i] = (time.perf_counter() - th) * 1e3
 
     wd.phase = "warm-up frames"
+    fixture = None
     for i in range(args.warmup):
         step(i)
+        if i == 0 and args.check and not sharded and not args.foreign and rank == 0:
+            torch.cuda.synchronize()  # frame 0 of the timed launch shape against the oracle's (untimed)
+            fixture = check_oracle_fixture(rt, args.config, W, H, bufs[0], rng)
     torch.cuda.synchronize()
     if sharded:
         dist.barrier()
@@ -957,12 +962,17 @@ def run(args):
             result["check"] = {"frames": n_total, "s": round(time.perf_counter() - t_chk, 2),
                                "against": "the same frames rendered unsharded in plain tile order (no cost order, "
                                           "no lane map) on this GPU, final surface compared bit for bit"}
+            if fixture is not None:
+                result["check_oracle_fixture"] = fixture
         if world == 1 and not args.no_cpu_baseline:
             auto_rows = {"cfg1": 256, "cfg2": 1080, "cfg3": 64, "cfg4": 540, "cfg5": 1080}[args.config]
             result["cpu_baseline"] = cpu_baseline_child(args.config, args.cpu_rows or auto_rows)
         print(json.dumps(result), flush=True)
         if args.check and not result["check_equal"]:
             print("bench.py: the timed frame differs from the unsharded plain render", file=sys.stderr, flush=True)
+            exit_code = 3
+        if fixture is not None and not fixture["equal"]:
+            print("bench.py: frame 0 of the timed launch shape differs from the oracle fixture", file=sys.stderr, flush=True)
             exit_code = 3
     if comm is not None:
         torch.cuda.synchronize()
@@ -992,6 +1002,37 @@ def foreign_copy(rt, scene):
             raise RuntimeError(rt.lib().rt_last_error().decode())
         setattr(f, k, p.value)
     return f
+
+
+FIXTURE = os.path.join(ROOT, "tests", "golden", "fullframe_oracle.json")
+
+
+def fixture_rows(a):
+    """Row hashes as tools/make_fullframe_golden.py makes them (NaN values as one canonical quiet NaN)."""
+    import hashlib
+    a = np.array(a, copy=True)
+    if a.dtype == np.float32:
+        a = a.view(np.uint32)
+        a[(a & 0x7FFFFFFF) > 0x7F800000] = 0x7FC00000
+    return [hashlib.sha256(np.ascontiguousarray(r).tobytes()).hexdigest()[:16] for r in a]
+
+
+def check_oracle_fixture(rt, cfg, W, H, surface, rng):
+    """Frame 0 of the timed launch shape itself (cost-ordered tiles, the measured lane map, the probed occupancy;
+    its first warm-up frame, from the seeded RNG states) against the CPU oracle's own full frame: the row hashes
+    of the frame and of every pixel's final RNG state in tests/golden/fullframe_oracle.json (data written once by
+    tools/make_fullframe_golden.py from oracle/rt_oracle.c).  None when there is no fixture for this config."""
+    if not os.path.exists(FIXTURE):
+        return None
+    g = json.load(open(FIXTURE)).get(cfg)
+    if not g or (g["width"], g["height"]) != (W, H):
+        return None
+    img = rt.surface_view(surface, W).cpu().numpy().reshape(H, W, 4)
+    st = rng.view(-1, 12)[:, :6].cpu().numpy().view(np.uint32).reshape(H, W, 6)
+    bad = sum(a != b for a, b in zip(fixture_rows(img), g["rows"]))
+    bad_rng = sum(a != b for a, b in zip(fixture_rows(st), g["rng_rows"]))
+    return {"equal": bad == 0 and bad_rng == 0, "frame": 0, "rows": H, "differing_rows": int(bad),
+            "differing_rng_rows": int(bad_rng), "against": "tests/golden/fullframe_oracle.json (the oracle's full frame 0)"}
 
 
 def check_unsharded(rt, scene_name, W, H, spp, bounces, frames, final):

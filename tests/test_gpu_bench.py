@@ -32,4 +32,6 @@ def test_bench_cfg2_line_is_bit_exact():
     assert line["check_equal"] is True
     assert line["check"]["frames"] == 3
     assert line["plan"]["kind"].startswith("cost")
+    # frame 0 of the exact timed launch shape against the oracle's own full frame (row hashes + RNG states)
+    assert line["check_oracle_fixture"]["equal"] is True, line["check_oracle_fixture"]
 
