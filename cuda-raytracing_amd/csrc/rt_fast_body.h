@@ -93,10 +93,13 @@ __device__ __forceinline__ bool shade_segment(const RenderArgs& a, const rtfast:
 // Instead XCD x takes runs of S = 2^v consecutive sub-tiles: its i-th workgroup renders
 // sub-tile ((i / S) * 8 + x) * S + i % S (a permutation of the first multiple of 8S workgroups;
 // the rest keep their index), so neighbouring pixels share an L2.  v = 5 (runs of 8 tiles,
-// 128x16 px): config 2 18.29 -> 17.73 ms; v = 4 17.8, v = 6 18.1, v = 1-3 18.1-18.3.
+// 128x16 px) in plain tile order: config 2 18.29 -> 17.73 ms; v = 4 17.8, v = 6 18.1, v = 1-3 18.1-18.3.
+// Round 6, on the final kernel with the cost-ordered lane map (whose consecutive waves are no longer
+// neighbours): v = 3 (runs of 8 sub-tiles) config 2 13.23-13.26 vs 13.41-13.49 ms, config 4 79.7-79.9 vs
+// 80.4-80.6 ms; v = 2 / 4 / the dispatcher's order in between (profiles/r06_ab_log.txt item 8).
 // RT_TUNE bits 16-19 override v; 15 keeps the dispatcher's order.
 __device__ __forceinline__ int xcd_block(uint32_t tune) {
-    const uint32_t g = blockIdx.x, tv = (tune >> 16) & 15u, v = tv ? tv : 5u;
+    const uint32_t g = blockIdx.x, tv = (tune >> 16) & 15u, v = tv ? tv : 3u;
     if (v == 15u) return (int)g;
     const uint32_t S = 1u << v, full = gridDim.x / (8u * S) * (8u * S);
     if (g >= full) return (int)g;
