@@ -803,8 +803,21 @@ def run(args):
         if args.backend == "nccl" and args.gather == "rccl":
             obj = [rt.Comm.unique_id() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
-            comm = rt.Comm(world, rank, obj[0])
-            gather_kind = "rt_gather_shards (RCCL send/recv group, librt_hip.so)"
+            comm_err = None
+            try:
+                comm = rt.Comm(world, rank, obj[0])
+            except rt.RTError as e:  # every rank must agree before any frame: MIN-reduce an ok flag
+                comm, comm_err = None, str(e)
+            ok = torch.tensor([0 if comm_err else 1], dtype=torch.int32, device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()):
+                gather_kind = "rt_gather_shards (RCCL send/recv group, librt_hip.so)"
+            else:  # the library's own communicator failed on some rank: gather through torch.distributed instead
+                if comm is not None:
+                    comm.close()
+                comm = None
+                gather_kind = f"torch.distributed.gather (nccl; rt_comm_init_rank failed: {comm_err or 'on another rank'})"
+                print(f"bench.py: rank {rank}: {gather_kind}", file=sys.stderr, flush=True)
         else:
             gather_kind = f"torch.distributed.gather ({args.backend})"
     recv_bytes = gather_layout(counts, lists.shape[1])[0] if sharded else None
