@@ -171,7 +171,7 @@ struct Stack {
     uint32_t* lds0;  // column 0's entry 0 (workgroup-uniform)
     uint32_t* ovf;   // this lane's entries SL, SL + 1, ...
     static constexpr int STEP = 4 * WGL;  // sp per entry
-    static __device__ __forceinline__ int depth(int sp) { return sp / STEP; }
+    static __device__ __forceinline__ int depth(int sp) { return (int)((uint32_t)sp / (uint32_t)STEP); }  // sp >= 0: a shift
     static __device__ __forceinline__ int column(int sp) { return (sp & (STEP - 1)) >> 2; }
     static __device__ __forceinline__ int empty(int col) { return 4 * col; }  // sp of an empty stack
     __device__ __forceinline__ uint32_t* at(int sp) const {
