@@ -1537,6 +1537,175 @@ __device__ __forceinline__ void pair_get_ray(const uint32_t* mail, int k, Ray& R
 }
 #endif
 
+#if defined(RT_GROUP)
+// ---------------------------------------------------------------------------------------
+// Group traversal (experiment, -DRT_GROUP = most rays): lone_traverse for 2-4 rays at
+// once.  When the small phase is down to n = 2..RT_GROUP rays and every other lane is done (no lane waits at a
+// big leaf), the wave splits into n groups: each ray's own lane (its OWNER) plus the done lanes dealt round
+// robin (MEMBERS; their ray and traversal registers are dead, their hit is not and is left alone).  Every
+// lane of a group holds the group's ray (copied once from the owner), current node, depth and closest
+// distance, and runs the inner steps' filtered-exact decisions itself; the group's stack is spread over its
+// members (member e holds entry e with its filtered tmin, as in lone_traverse), so a pop is one ballot and
+// the highest passing member of the group; the owner alone tests a small leaf (pair_test, its own hit) and
+// the group's distance follows by a permute.  Any group reaching a big leaf, or a push its members cannot
+// hold, ends group mode for all: stacks go back to the owners' LDS columns, the big-leaf rounds take over.
+// The same steps in the same order per ray: bit-exact by construction.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bperm(uint32_t v, int src) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
+__device__ __forceinline__ float bpermf(float v, int src) { return __uint_as_float(bperm(__float_as_uint(v), src)); }
+__device__ __forceinline__ uint32_t rank_in(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+#if defined(RT_GROUP_CALL)  // a real call: the trace loop's register allocation stays the production one
+#define RT_GROUP_INLINE __attribute__((noinline))
+#else
+#define RT_GROUP_INLINE __forceinline__
+#endif
+template <class S>
+__device__ RT_GROUP_INLINE void group_traverse(const float4* nodes4, const float4* spairs, const S& stk,
+                                               unsigned long long mS, Ray& R, Hit& h, Trav& T, bool& active) {
+    constexpr int SL = S::LDS_ENTRIES;
+    const int lane = (int)(threadIdx.x & 63u);
+    const uint32_t n = (uint32_t)__popcll(mS);
+    const bool owner = ((mS >> lane) & 1ull) != 0;
+    const uint32_t mrank = rank_in(~mS);
+    const uint32_t gid = owner ? rank_in(mS) : mrank % n;
+    const int eidx = owner ? -1 : (int)(mrank / n);
+    const int cap = min((int)((64u - n) / n), SL);  // entries every group's members can hold, all in LDS at exit
+    // the owners' lanes (wave-uniform), then this lane's group owner and group mask
+    unsigned long long rest = mS, gm = 0;
+    int ol = lane;
+    for (uint32_t k = 0; k < n; k++) {
+        const int lk = __ffsll((long long)rest) - 1;
+        rest &= rest - 1;
+        const unsigned long long mk = __ballot(gid == k);
+        if (gid == k) ol = lk, gm = mk;
+    }
+    // the group's ray, node, depth and closest distance from its owner (members' ray registers are dead)
+    R.o = rtm::mk(bpermf(R.o.x, ol), bpermf(R.o.y, ol), bpermf(R.o.z, ol));
+    R.d = rtm::mk(bpermf(R.d.x, ol), bpermf(R.d.y, ol), bpermf(R.d.z, ol));
+    R.nd = rtm::mk(bpermf(R.nd.x, ol), bpermf(R.nd.y, ol), bpermf(R.nd.z, ol));
+    R.r = rtm::mk(bpermf(R.r.x, ol), bpermf(R.r.y, ol), bpermf(R.r.z, ol));
+    R.fast = bperm(R.fast ? 1u : 0u, ol) != 0u;
+    uint32_t cf = bperm(T.first, ol), cc = bperm(T.count, ol);
+    const int osp = (int)bperm((uint32_t)T.sp, ol);
+    const int ocol = S::column(osp);
+    int gd = S::depth(osp);
+    float gb = bpermf(h.best, ol);
+    uint32_t* const col = stk.lds0 + ocol;
+    // member e: entry e of its group's stack, with its filtered tmin (lone_traverse's entry state)
+    uint32_t e_idx = 0, e_first = 0, e_count = 0;
+    float e_tmin = 0.0f;
+    bool e_exact = false;
+    if (eidx >= 0 && eidx < gd) {
+        e_idx = col[eidx * S::LANES];
+        const float4 lo = ldo(nodes4, 2 * e_idx), hi = ldo(nodes4, 2 * e_idx + 1);
+        float tx;
+        if (R.fast) {
+            slab_approx(R, lo, hi, &e_tmin, &tx);
+        } else {
+            slab_exact(R, lo, hi, &e_tmin, &tx);
+            e_exact = true;
+        }
+        e_first = __float_as_uint(hi.z), e_count = __float_as_uint(hi.w);
+    }
+    bool gdone = false;  // this lane's group: its ray's traversal is over
+    for (;;) {
+        bool do_pop = false, leave = false;
+        if (!gdone) {
+            if (cc == 0) {
+                if (gd >= cap) {
+                    leave = true;  // a push might not fit the members: back to per-lane steps
+                } else {
+                    const float4 l0 = ldo(nodes4, 2 * cf), l1 = ldo(nodes4, 2 * cf + 1);
+                    const float4 r0 = ldo(nodes4, 2 * cf + 2), r1 = ldo(nodes4, 2 * cf + 3);
+                    float tl = 0.0f, tlx = 0.0f, tr = 0.0f, trx = 0.0f;
+                    int okl = UNSURE, okr = UNSURE, rlt = UNSURE;
+                    if (R.fast) {
+                        slab_approx(R, l0, l1, &tl, &tlx);
+                        slab_approx(R, r0, r1, &tr, &trx);
+                        okl = classify_ok(tl, tlx);
+                        okr = classify_ok(tr, trx);
+                        rlt = okr == YES ? classify_lt(tr, gb) : NO;
+                    }
+                    bool exact_l = false;
+                    if (okl == UNSURE || okr == UNSURE || rlt == UNSURE) {
+                        slab_exact(R, l0, l1, &tl, &tlx);
+                        slab_exact(R, r0, r1, &tr, &trx);
+                        okl = (tlx >= tl && tlx > 0.0f) ? YES : NO;
+                        okr = (trx >= tr && trx > 0.0f) ? YES : NO;
+                        rlt = (okr == YES && tr < gb) ? YES : NO;
+                        exact_l = true;
+                    }
+                    if (rlt == YES) {
+                        if (okl == YES) {
+                            if (eidx == gd) e_idx = cf, e_tmin = tl, e_exact = exact_l, e_first = __float_as_uint(l1.z),
+                                            e_count = __float_as_uint(l1.w);
+                            gd++;
+                        }
+                        cf = __float_as_uint(r1.z), cc = __float_as_uint(r1.w);
+                    } else {
+                        bool llt = false;
+                        if (okl == YES) {
+                            int cl = exact_l ? (tl < gb ? YES : NO) : classify_lt(tl, gb);
+                            if (cl == UNSURE) {
+                                float te, tx;
+                                slab_exact(R, l0, l1, &te, &tx);
+                                cl = te < gb ? YES : NO;
+                            }
+                            llt = cl == YES;
+                        }
+                        if (llt) cf = __float_as_uint(l1.z), cc = __float_as_uint(l1.w);
+                        else do_pop = true;
+                    }
+                }
+            } else if (cc <= (uint32_t)BIG) {
+                if (owner)  // the small leaf, in leaf order, on the owner's own hit
+                    for (uint32_t i = cf; i < cf + cc; i += 2) pair_test(R, ld_pair(spairs, i), h);
+                do_pop = true;
+            } else {
+                leave = true;  // a big leaf: the wave's big-leaf rounds
+            }
+        }
+        gb = bpermf(h.best, ol);  // (owners' distances; members' own hits untouched)
+        if (__ballot(leave)) break;
+        // pops: members holding live entries test them; the group continues at its highest passing entry
+        int cl = NO;
+        if (!gdone && do_pop && eidx >= 0 && eidx < gd) {
+            cl = e_exact ? (e_tmin < gb ? YES : NO) : classify_lt(e_tmin, gb);
+            if (cl == UNSURE) {
+                const float4 lo = ldo(nodes4, 2 * e_idx), hi = ldo(nodes4, 2 * e_idx + 1);
+                float tx;
+                slab_exact(R, lo, hi, &e_tmin, &tx);
+                e_exact = true;
+                cl = e_tmin < gb ? YES : NO;
+            }
+        }
+        const unsigned long long P = __ballot(cl == YES) & gm;
+        const int w = P ? 63 - __clzll((long long)P) : lane;
+        const uint32_t wf = bperm(e_first, w), wc = bperm(e_count, w), we = bperm((uint32_t)eidx, w);
+        if (!gdone && do_pop) {
+            if (P) {
+                cf = wf, cc = wc, gd = (int)we;
+            } else {
+                gdone = true;
+                if (owner) active = false;
+            }
+        }
+        if (!__ballot(!gdone)) break;
+    }
+    // back to per-lane state: the owners of unfinished rays take the group's node and depth, the members
+    // put their entries back into the owner's LDS column (gd <= cap <= the LDS rows)
+    if (!gdone) {
+        if (owner) T.first = cf, T.count = cc, T.sp = S::empty(ocol) + gd * S::STEP;
+        if (eidx >= 0 && eidx < gd) col[eidx * S::LANES] = e_idx;
+    }
+}
+#endif
+
 // BVHRayHit for one lane (`live` = the lane has a segment to trace), every lane of the wave
 // calling.  Small steps run while any lane has one; big leaves wait until every lane is done
 // or waiting at one.  MODE & 3 -- 0: big leaves through pair records (shared-leaf loop and
@@ -1660,6 +1829,16 @@ __device__ __forceinline__ void trace(const float4* nodes4, const float4* tris, 
             const unsigned long long mI = __ballot(inner), mL = __ballot(leafs);
             if (mI | mL) {
                 const uint32_t nI = (uint32_t)__popcll(mI), nL = (uint32_t)__popcll(mL);
+#if defined(RT_GROUP)
+                if constexpr (!STATS && !scr_on && (MODE & 4) == 0) {
+                    const uint32_t ng = nI + nL;
+                    if (ng >= 2 && ng <= (uint32_t)RT_GROUP && (mI | mL) == __ballot(active) && spairs &&
+                        !__ballot((inner || leafs) && S::depth(T.sp) >= min((int)((64u - ng) / ng), S::LDS_ENTRIES))) {
+                        group_traverse(nodes4, spairs, stk, mI | mL, R, h, T, active);
+                        continue;
+                    }
+                }
+#endif
                 if constexpr (!STATS) {
                     // one lane left in the small phase: the whole wave runs its DFS (lone_traverse),
                     // when its stack lives in LDS (RT_TUNE bit 26 turns this off); a lane that must
